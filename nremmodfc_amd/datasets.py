@@ -1,0 +1,32 @@
+"""Input data of the reference, shipped as exact .npy copies (nremmodfc_amd/data/).
+
+SC_opti_25julio.txt (structural connectome, loaded at whole_sweep_both.py:34),
+empirical/mean_mat_{W,N1,N2,N3}_8dic24.txt (empirical FC, whole_sweep_both.py:36-37)
+and empirical/maps/*.npy (NA/ACh proxy maps, whole_sweep_both_maps.py:44-65).
+The SHUFFLED_*_LABELS_*.npy files of the reference are pickled object arrays and
+are not shipped (nothing on the hot path reads them).
+"""
+import os
+
+import numpy as np
+
+DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+STATES = ("W", "N1", "N2", "N3")
+
+# whole_sweep_both_maps.py:35-41 / run_many_seeds.py:66-72
+MAPNAMES_ACH = ["HOMO", "DIST_VAChT_feobv_hc18_aghourian", "SHUFFLED_SYMM_DIST_VAChT_feobv_hc18_aghourian"]
+MAPNAMES_NA = ["HOMO", "DIST_LC_proj", "SHUFFLED_SYMM_DIST_LC_proj"]
+
+
+def load_sc():
+    return np.load(os.path.join(DATA, "SC_opti_25julio.npy"))
+
+
+def load_empfc(state):
+    return np.load(os.path.join(DATA, f"mean_mat_{state}_8dic24.npy"))
+
+
+def load_map(name, n=90):
+    """Map normalised to mean 1 (whole_sweep_both_maps.py:47-57); HOMO = ones."""
+    m = np.ones(n) if name == "HOMO" else np.load(os.path.join(DATA, name + ".npy")).astype(np.float64)
+    return m / m.mean()

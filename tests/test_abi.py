@@ -1,0 +1,50 @@
+"""libwcsde.so builds, loads and exports every symbol include/wcsde.h declares (no GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "wcsde.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", src)) - {"if", "sizeof", "defined"})
+
+
+def test_header_parses():
+    fns = header_functions()
+    assert "wc_integrate" in fns and "wc_last_error" in fns
+
+
+def test_library_exports_header_symbols():
+    from nremmodfc_amd import _build, _lib
+    _build.build()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in header_functions():
+        assert hasattr(lib, name), name
+
+
+def test_abi_version_and_workspace():
+    from nremmodfc_amd import _lib
+    L = _lib.lib()
+    assert L.wcsde_abi_version() == 1
+    assert L.wc_workspace_size(90, _lib.WC_F32) == 6 * 6 * 64 * 4 * 4
+    assert L.wc_workspace_size(90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
+    assert L.wc_workspace_size(16, _lib.WC_F32) == 64 * 4 * 4
+
+
+def test_invalid_arguments_fail_loudly():
+    """Argument validation happens before any device work (runs without a GPU)."""
+    from nremmodfc_amd import _lib
+    L = _lib.lib()
+    p = _lib.WCParamsC()
+    rc = L.wc_integrate(ctypes.byref(p), 0, 0, 90, *([None] * 7), 0, 1, 1.0, 0, None, None, None,
+                        None, 0, None)
+    assert rc == -1
+    assert b"invalid" in L.wc_last_error()
+    rc = L.wc_integrate(ctypes.byref(p), 0, 4, 200, *([ctypes.c_void_p(16)] * 7), 0, 1, 1.0, 0,
+                        None, None, None, ctypes.c_void_p(16), 1 << 20, None)
+    assert rc == -2

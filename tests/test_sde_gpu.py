@@ -1,0 +1,150 @@
+"""HIP integrator (libwcsde.so) vs the CPU oracle at fixed Philox keys.
+
+Tolerances (north_star: "within a stated fp64->fp32 tolerance at fixed seed"):
+  * noise, fp64: rtol 1e-12 (libm vs ocml transcendentals);
+  * noise, fp32: |dz| <= 2e-3 worst case (v_log_f32 near u=1 feeds a sqrt),
+    rms <= 2e-6;
+  * trajectories over the short horizons below, fp64: max |dE| <= 1e-9;
+  * fp32 (E, I, coupling in fp32, a_ie in fp64): max |dE| <= 2e-3 and
+    rms <= 2e-4 over the same horizons.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from nremmodfc_amd import _lib, datasets
+from nremmodfc_amd.model import Batch, driver_params, sim_keys
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_noise(keys, step, N, prec):
+    B = len(keys)
+    dt = torch.float64 if prec == "f64" else torch.float32
+    out = torch.empty((B, N), dtype=dt, device="cuda")
+    k = torch.from_numpy(np.asarray(keys, dtype=np.uint64).view(np.int64).copy()).cuda()
+    rc = _lib.lib().wc_noise(_lib.WC_F64 if prec == "f64" else _lib.WC_F32, B, N, _lib.ptr(k), step,
+                             _lib.ptr(out), _lib.stream_handle())
+    _lib.check(rc, "wc_noise")
+    torch.cuda.synchronize()
+    return out.double().cpu().numpy()
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_noise_matches_oracle(cuda, prec):
+    keys = sim_keys(list(range(8)) + [2**31 + 5], [0, 1, 2, 3, 4, 5, 6, 7, 123456])
+    N = 90
+    for step in (0, 1, 19, 123456, 2**33 + 7):
+        got = gpu_noise(keys, step, N, prec)
+        ref = np.stack([oracle.step_normals(int(k), step, N) for k in keys])
+        if prec == "f64":
+            np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-13)
+        else:
+            d = np.abs(got - ref)
+            assert d.max() <= 2e-3 and np.sqrt(np.mean(d ** 2)) <= 2e-6, (d.max(), np.sqrt(np.mean(d ** 2)))
+
+
+def run_pair(sc, G, sig, keys, n1, n2, n3, rec_every, prec, params=None):
+    p = params or driver_params()
+    gb = Batch(sc, G, sig, keys, p, precision=prec)
+    ob = oracle.OracleBatch(sc, G, sig, keys, p)
+    for n, tau in ((n1, 0.05), (n2, 1.0)):
+        if n:
+            gb.integrate(n, tau)
+            ob.integrate(n, tau)
+    n_rec = -(-n3 // rec_every)
+    rec = torch.empty((n_rec, gb.B, gb.N), dtype=gb.rec_dtype, device="cuda")
+    recI = torch.empty_like(rec)
+    gb.integrate(n3, 2.0, rec_every, rec, recI)
+    orec = ob.integrate(n3, 2.0, rec_every)
+    torch.cuda.synchronize()
+    g = rec.double().cpu().numpy().transpose(1, 0, 2)  # -> [B][n_rec][N]
+    return g, orec, gb, ob, recI
+
+
+def tol(prec):
+    return (1e-9, 1e-10) if prec == "f64" else (2e-3, 2e-4)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_homogeneous_sweep_cells(cuda, sc90, prec):
+    """16 cells of the shipped (dG, dsigma) grid, 2 seeds each = 2 waves + a tail of 5."""
+    dG = np.linspace(-0.1, 0.3, 20, endpoint=False)[::5]
+    ds = np.linspace(-0.2, 0.2, 20, endpoint=False)[::5]
+    cells = [(a, b) for a in dG for b in ds]
+    G = np.array([0.16 + a for a, b in cells] * 2 + [0.16] * 5)
+    S = np.array([7.68 + b for a, b in cells] * 2 + [7.68] * 5)
+    keys = sim_keys([0] * 16 + [1] * 16 + [2] * 5, list(range(16)) * 2 + [0] * 5)
+    g, o, gb, ob, _ = run_pair(sc90, G, S, keys, 300, 300, 600, 20, prec)
+    mx, rms = tol(prec)
+    d = np.abs(g - o)
+    assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
+    for x, y in ((gb.E, ob.E), (gb.I, ob.I), (gb.A, ob.A)):
+        dd = np.abs(x.cpu().numpy() - y)
+        assert dd.max() <= mx, dd.max()
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_maps_heterogeneous_params(cuda, sc90, prec):
+    """Per-node G_i = G + dG*m_ach_i, sigma_i = s + ds*m_na_i (whole_sweep_both_maps.py:104-108)."""
+    ach = datasets.load_map("DIST_VAChT_feobv_hc18_aghourian")
+    na = datasets.load_map("DIST_LC_proj")
+    dGs = np.array([-0.1, 0.0, 0.18, 0.28])
+    dss = np.array([-0.2, -0.12, 0.0, 0.18])
+    G = np.stack([0.16 + a * ach for a in dGs for b in dss])
+    S = np.stack([7.68 + b * na for a in dGs for b in dss])
+    keys = sim_keys(list(range(16)), [7] * 16)
+    g, o, *_ = run_pair(sc90, G, S, keys, 200, 200, 400, 20, prec)
+    mx, rms = tol(prec)
+    d = np.abs(g - o)
+    assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
+
+
+@pytest.mark.parametrize("N,B", [(16, 1), (20, 17), (33, 40), (64, 16), (90, 3)])
+def test_shapes_and_tails(cuda, N, B):
+    rng = np.random.default_rng(N)
+    sc = rng.uniform(size=(N, N)) * (rng.uniform(size=(N, N)) < 0.4)
+    sc = (sc + sc.T) / 2
+    np.fill_diagonal(sc, 0)
+    sc *= 2.51 / sc.sum(1).mean()
+    keys = sim_keys(list(range(B)), [N] * B)
+    g, o, *_ = run_pair(sc, 0.16, 7.68, keys, 100, 0, 200, 20, "f64")
+    assert np.abs(g - o).max() <= 1e-9
+
+
+def test_recording_I_and_chunking(cuda, sc90):
+    """Chunked calls (step0 advancing) equal one long call; recI holds I."""
+    keys = sim_keys([4, 5], [0, 0])
+    a = Batch(sc90, 0.16, 7.68, keys, precision="f64")
+    recE = torch.empty((10, 2, 90), dtype=torch.float64, device="cuda")
+    recI = torch.empty_like(recE)
+    a.integrate(200, 2.0, 20, recE, recI)
+    b = Batch(sc90, 0.16, 7.68, keys, precision="f64")
+    parts = []
+    for _ in range(4):
+        r = torch.empty((3, 2, 90), dtype=torch.float64, device="cuda")
+        b.integrate(50, 2.0, 20, r)  # records local steps 0, 20, 40 of each 50-step chunk
+        parts.append(r)
+    torch.cuda.synchronize()
+    assert torch.equal(a.E, b.E) and torch.equal(a.A, b.A)
+    assert torch.equal(recE[0], parts[0][0]) and torch.equal(recE[1], parts[0][1])
+    ob = oracle.OracleBatch(sc90, 0.16, 7.68, keys, driver_params())
+    for k in range(10):
+        assert np.abs(recI[k].cpu().numpy() - ob.I).max() <= 1e-12
+        ob.integrate(20, 2.0)
+
+
+def test_f32_tracks_f64_statistics(cuda, sc90):
+    """fp32 fast path vs fp64 over 100k steps: same mean activity per node (pathwise may drift)."""
+    keys = sim_keys(list(range(16)), [0] * 16)
+    out = {}
+    for prec in ("f32", "f64"):
+        b = Batch(sc90, 0.16, 7.68, keys, precision=prec)
+        b.integrate(10_000, 0.05)
+        rec = torch.empty((2500, 16, 90), dtype=b.rec_dtype, device="cuda")
+        b.integrate(50_000, 2.0, 20, rec)
+        out[prec] = rec.double().mean(0).cpu().numpy()
+    assert np.abs(out["f32"] - out["f64"]).max() < 0.02
