@@ -29,6 +29,18 @@ extern "C" {
 
 #define WCSDE_ABI_VERSION 1
 
+/* Noise stream (the reference's numba RNG is seeded from os.urandom and never
+ * reproducible; the build defines its own): Philox4x32-10 with
+ * key (WC_PHILOX_KEY0, WC_PHILOX_KEY1) and counter
+ *   (step & 0xffffffff, ((step >> 32) << 16) | quad, simkey lo32, simkey hi32)
+ * for global Euler step `step` (< 2^48), node quad `quad` = node / 4 (< 2^16)
+ * and the 64-bit per-simulation key; outputs x0..x3 ->
+ *   u = (2*(x >> 9) + 1) * 2^-24,
+ *   z[4q+0,1] = sqrt(-2 ln u0) (cos, sin)(2 pi u1),  z[4q+2,3] likewise from u2, u3,
+ * and the noise of wc:80 is sqdtD * z. */
+#define WC_PHILOX_KEY0 0x243F6A88u
+#define WC_PHILOX_KEY1 0x85A308D3u
+
 enum wc_precision { WC_F32 = 0, WC_F64 = 1 };
 
 enum wc_error {
@@ -54,7 +66,8 @@ typedef struct wc_params {
 int wcsde_abi_version(void);
 const char* wc_last_error(void);
 
-/* Bytes of device workspace wc_integrate needs for an N-node connectome. */
+/* Bytes of device workspace wc_integrate needs for an N-node connectome (the
+ * connectome's MFMA A-operand image, rebuilt by every call). */
 size_t wc_workspace_size(int N, int precision);
 
 /*
@@ -75,7 +88,9 @@ size_t wc_workspace_size(int N, int precision);
  *            s % rec_every == 0 (wc:124-125) at row s/rec_every of recE/recI/recA,
  *            layout [n_rec][B][N], element type float (WC_F32) or double (WC_F64);
  *            recI/recA may be NULL.  rec_every == 0: no recording.
- *  precision WC_F32: E,I and coupling in fp32, a_ie accumulated in fp64;
+ *  precision WC_F32: E, I, sigmoids in fp32; coupling as six bf16 MFMA cross
+ *            terms of 3-way split operands with fp32 accumulation (fp32-
+ *            equivalent); a_ie as a compensated fp32 pair;
  *            WC_F64: everything fp64 (the parity mode).
  */
 int wc_integrate(const wc_params* p, int precision, int B, int N,
@@ -89,6 +104,16 @@ int wc_integrate(const wc_params* p, int precision, int B, int N,
  * (float or double per precision).  Test hook for the noise stream. */
 int wc_noise(int precision, int B, int N, const uint64_t* keys, int64_t step,
              void* out, void* stream);
+
+/* Diagnostic: wc_integrate (WC_F32, no recI/recA) through compile-time kernel
+ * variant `variant` (ablations / alternative tilings, see wc_sde.hip
+ * launch_diag); 81 <= N <= 96 only.  Not part of the product path. */
+int wc_diag_integrate(int variant, const wc_params* p, int B, int N,
+                      const double* sc, const double* G, const double* sigmaE,
+                      const uint64_t* keys, double* E, double* I, double* A,
+                      int64_t step0, int64_t nsteps, double tau_ip,
+                      int64_t rec_every, void* recE,
+                      void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

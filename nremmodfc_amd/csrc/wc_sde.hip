@@ -3,21 +3,25 @@
 // Replaces the numba hot loop of netwWilsonCowanPlastic.py (wilsonCowan
 // wc:77-83, run wc:86-137) for a whole batch of (G, sigmaE, seed) simulations.
 //
-// Layout (DESIGN.md "Kernel 1"): one wave64 integrates 16 simulations.  Lane
-// l = 16*g + j owns simulation j of the wave and, for every 16-node tile t,
-// the four nodes 16t + 4g + r (r = 0..3) -- E, I, a_ie live in registers for
-// the whole launch.  That register layout is simultaneously
-//   * the C/D layout of the coupling MFMA  D[node][sim] = CM . E^T  and
-//   * the B-operand layout of the next step's MFMA (k-step (t, r) feeds
-//     register (t, r) of every lane),
-// so the dense SC@E contraction moves no data between lanes, LDS or HBM:
-// the matrix pipe is the data movement.  The connectome is the A operand,
-// pre-arranged once per launch in an LDS fragment image (conflict-free
-// ds_read_b128, one 16-B chunk per lane per (out tile, k tile)).
-//   fp32: v_mfma_f32_16x16x4_f32 (exact f32 fma chain)
-//   fp64: v_mfma_f64_16x16x4_f64 (C/D rows permuted by sigma(rho), below)
-// The elementwise update (two logistic sigmoids, plasticity, Philox4x32-10
-// noise + Box-Muller) runs on the VALU between the MFMAs.
+// Layout (DESIGN.md "Kernel 1").  A workgroup of NW waves integrates 16
+// simulations.  Lane l = 16*g + j of every wave serves simulation j; wave w
+// owns the OT = NT/NW node tiles T0 = w*OT .. T0+OT-1, and within tile t lane
+// group g owns nodes 16t + 4g + r (r = 0..3): E, I, a_ie, G, sigmaE of those
+// nodes live in registers for the whole launch.  That layout is at once
+//   * the C/D layout of the coupling MFMA  D[node][sim] = CM . E^T, and
+//   * the B-operand layout of the next step's MFMA,
+// so SC@E needs no lane shuffles: each wave publishes its new E tiles to a
+// double-buffered LDS image (lane-to-lane copy), one s_barrier, and every wave
+// streams the whole E vector back from LDS as MFMA B operands.
+//
+// Coupling arithmetic:
+//   fp32 product path (V_BF16X6): E and CM are split into three bf16 parts
+//     (hi + mid + lo, |x - sum| <= 2^-27 |x|) and the six cross terms of weight
+//     >= 2^-18 run on v_mfma_f32_16x16x32_bf16 with fp32 accumulation -- fp32-
+//     equivalent accuracy at 2.7x the rate of v_mfma_f32_16x16x4_f32.
+//   fp64 parity path: v_mfma_f64_16x16x4_f64 (rows permuted, Tr<double>).
+// The elementwise update (two logistic sigmoids, homeostatic plasticity,
+// Philox4x32-10 noise + Box-Muller) runs on the VALU beside the MFMAs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -32,42 +36,72 @@ int set_err(int code, const char* msg) {
     return code;
 }
 
-constexpr int kWaves = 4;              // waves per workgroup
-constexpr int kSimsPerWave = 16;
-constexpr int kSimsPerBlock = kWaves * kSimsPerWave;
-constexpr int kMaxTiles = 6;           // N <= 96 on the register-resident path
+constexpr int kSims = 16;     // simulations per workgroup (MFMA N dimension)
+constexpr int kMaxTiles = 6;  // N <= 96 on the register-resident path
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-// ---------------- Philox4x32-10 (must match oracle/wc_oracle.c) ----------------
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                              uint32_t k0, uint32_t k1, uint32_t out[4]) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+// ---------------- noise: Philox4x32-10 (must match oracle/wc_oracle.c) ----------------
+// key = (WC_PHILOX_KEY0, WC_PHILOX_KEY1) for every simulation (wave-uniform: the
+// key schedule lives in SGPRs); counter = (step lo32, (step hi16 << 16) | quad,
+// simkey lo32, simkey hi32).  Outputs feed two Box-Muller pairs -> the standard
+// normals of nodes 4*quad + 0..3.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
+}
+
+__device__ __forceinline__ void mul_wide(uint32_t a, uint32_t m, uint32_t& hi, uint32_t& lo) {
+    uint64_t r;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "s"(m) : "vcc");  // one op for hi:lo
+    hi = (uint32_t)(r >> 32);
+    lo = (uint32_t)r;
+}
+
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
+    uint32_t k0 = WC_PHILOX_KEY0, k1 = WC_PHILOX_KEY1;
+    // round 1: c0 (the step) is wave-uniform -> scalar multiply
+    {
         const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
         const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        c0 = hi1 ^ c1 ^ k0;
+        c0 = xor3(hi1, c1, k0);
         c1 = lo1;
-        c2 = hi0 ^ c3 ^ k1;
+        c2 = xor3(hi0, c3, k1);
+        c3 = lo0;
+    }
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+        uint32_t hi0, lo0, hi1, lo1;
+        mul_wide(c0, 0xD2511F53u, hi0, lo0);
+        mul_wide(c2, 0xCD9E8D57u, hi1, lo1);
+        c0 = xor3(hi1, c1, k0);
+        c1 = lo1;
+        c2 = xor3(hi0, c3, k1);
         c3 = lo0;
     }
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-// u = (2*(x>>9)+1) * 2^-24, exact in fp32/fp64, in (0,1)
+__device__ __forceinline__ void philox_ctr(uint64_t step, uint32_t quad, uint64_t simkey, uint32_t out[4]) {
+    philox((uint32_t)step, ((uint32_t)(step >> 32) << 16) | quad, (uint32_t)simkey, (uint32_t)(simkey >> 32),
+           out);
+}
+
+// u = (2*(x>>9)+1) * 2^-24, exact in fp32 and fp64, in (0,1)
 __device__ __forceinline__ float u01f(uint32_t x) { return (float)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8f; }
 __device__ __forceinline__ double u01d(uint32_t x) { return (double)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8; }
 
-// Box-Muller normals of nodes 4q..4q+3 -- fp32 hardware transcendentals
-__device__ __forceinline__ void quad_normals(uint32_t s_lo, uint32_t s_hi, uint32_t q, uint32_t k0,
-                                             uint32_t k1, float z[4]) {
+// fp32: hardware transcendentals.  ln u = log2(u) ln2; v_sin/v_cos take
+// revolutions (sin(2 pi x)).  Inputs are never denormal: u >= 2^-24.
+__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, float z[4]) {
     uint32_t x[4];
-    philox4x32_10(s_lo, s_hi, q, 0u, k0, k1, x);
-    // ln(u) = log2(u) * ln2 ; v_sin/v_cos take revolutions: sin(2*pi*u)
-    const float r0 = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[0])));
-    const float r1 = __builtin_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[2])));
+    philox_ctr(step, q, key, x);
+    const float r0 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[0])));
+    const float r1 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[2])));
     const float a0 = u01f(x[1]), a1 = u01f(x[3]);
     z[0] = r0 * __builtin_amdgcn_cosf(a0);
     z[1] = r0 * __builtin_amdgcn_sinf(a0);
@@ -75,13 +109,13 @@ __device__ __forceinline__ void quad_normals(uint32_t s_lo, uint32_t s_hi, uint3
     z[3] = r1 * __builtin_amdgcn_sinf(a1);
 }
 
-__device__ __forceinline__ void quad_normals(uint32_t s_lo, uint32_t s_hi, uint32_t q, uint32_t k0,
-                                             uint32_t k1, double z[4]) {
+// fp64: correctly rounded-ish libm (ocml); sincospi reduces 2u exactly
+__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, double z[4]) {
     uint32_t x[4];
-    philox4x32_10(s_lo, s_hi, q, 0u, k0, k1, x);
+    philox_ctr(step, q, key, x);
     const double r0 = sqrt(-2.0 * log(u01d(x[0])));
     const double r1 = sqrt(-2.0 * log(u01d(x[2])));
-    double s0, c0, s1, c1;  // sin/cos(2*pi*u) with exact pi-reduction
+    double s0, c0, s1, c1;
     sincospi(2.0 * u01d(x[1]), &s0, &c0);
     sincospi(2.0 * u01d(x[3]), &s1, &c1);
     z[0] = r0 * c0;
@@ -102,7 +136,7 @@ template <> struct Tr<float> {
         return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((mu - x) * sl));
     }
     __device__ static __forceinline__ float slope(double s) { return (float)(s * 1.4426950408889634); }
-    // output row rho of an f32 16x16x4 tile is (lane>>4)*4 + reg: identity map
+    // C/D row of a 16x16x4 f32 tile is (lane>>4)*4 + reg: identity row->node map
     __host__ __device__ static __forceinline__ int row_node(int rho) { return rho; }
 };
 template <> struct Tr<double> {
@@ -120,7 +154,6 @@ template <> struct Tr<double> {
 };
 
 struct KArgs {
-    // model constants
     double a_ee, a_ei, a_ii, tauE, tauI, P, rhoE, rE, rI, mu, sigmaI, sqdtD, dtSim;
     double tau_ip;
     const double* G;
@@ -129,7 +162,7 @@ struct KArgs {
     double* E;
     double* I;
     double* A;
-    const void* frag;  // [NT*NT][64][4] Real
+    const void* frag;  // A-operand image (build_frag / build_frag_bf16)
     void* recE;
     void* recI;
     void* recA;
@@ -139,144 +172,346 @@ struct KArgs {
     int B, N;
 };
 
-// Build the A-operand fragment image: frag[(T*NT + t)*64 + lane][r] =
-//   CM[16T + row_node(lane&15)][16t + 4(lane>>4) + r]   (0 outside N)
+// ---------------- A-operand (connectome) images ----------------
+// native MFMA: frag[(T*NT + t)*64 + lane][r] = CM[16T + row_node(lane&15)][16t + 4(lane>>4) + r]
 template <typename Real, int NT>
 __global__ void build_frag(const double* __restrict__ sc, int N, Real* __restrict__ frag) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int total = NT * NT * 64 * 4;
-    if (idx >= total) return;
+    if (idx >= NT * NT * 64 * 4) return;
     const int r = idx & 3;
     const int lane = (idx >> 2) & 63;
-    const int tt = idx >> 8;  // T*NT + t
+    const int tt = idx >> 8;
     const int T = tt / NT, t = tt % NT;
     const int row = 16 * T + Tr<Real>::row_node(lane & 15);
     const int col = 16 * t + 4 * (lane >> 4) + r;
     frag[idx] = (row < N && col < N) ? (Real)sc[(size_t)row * N + col] : (Real)0;
 }
 
-// kHoist: let the compiler keep the whole fragment image in registers across
-// the step loop (f32, 1 wave/SIMD); otherwise re-read it from LDS every step.
-template <typename Real, int NT, bool kHoist>
-__global__ void __launch_bounds__(kWaves * 64) wc_sde_kernel(const KArgs a) {
+// bf16x6: frag[((T*NC + c)*3 + p)*64 + lane][jj] = part p of
+//   CM[16T + (lane&15)][16(2c + jj/4) + 4(lane>>4) + jj%4]    (k-chunk c = tiles 2c, 2c+1)
+// (the B operand of chunk c, lane l, element jj is E of that same node)
+template <int NT>
+__global__ void build_frag_bf16(const double* __restrict__ sc, int N, bf16x8* __restrict__ frag) {
+    constexpr int NC = NT / 2;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= NT * NC * 64) return;
+    const int lane = idx & 63;
+    const int tc = idx >> 6;
+    const int T = tc / NC, c = tc % NC;
+    const int row = 16 * T + (lane & 15);
+    bf16x8 part[3];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        const int col = 16 * (2 * c + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);
+        const double x = (row < N && col < N) ? sc[(size_t)row * N + col] : 0.0;
+        const __bf16 h = (__bf16)(float)x;
+        const double r1 = x - (double)(float)h;
+        const __bf16 m = (__bf16)(float)r1;
+        part[0][jj] = h;
+        part[1][jj] = m;
+        part[2][jj] = (__bf16)(float)(r1 - (double)(float)m);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) frag[(size_t)(tc * 3 + p) * 64 + lane] = part[p];
+}
+
+// v = hi + mid + lo, each a bf16: |v - hi - mid - lo| <= 2^-27 |v|
+__device__ __forceinline__ void split3(const float v[4], bf16x4& hi, bf16x4& mid, bf16x4& lo) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const __bf16 h = (__bf16)v[i];
+        const float r = v[i] - (float)h;
+        const __bf16 m = (__bf16)r;
+        hi[i] = h;
+        mid[i] = m;
+        lo[i] = (__bf16)(r - (float)m);
+    }
+}
+
+// ---------------- variants ----------------
+enum : int {
+    V_FRAG_REGS = 1,  // A-operand fragments held in registers (else streamed from LDS each step)
+    V_NO_RNG = 2,     // ablation: noise term zero
+    V_NO_MFMA = 4,    // ablation: coupling skipped
+    V_KAHAN_A = 8,    // fp32: a_ie as a compensated fp32 pair instead of fp64
+    V_BF16X6 = 32,    // fp32 coupling as the six bf16 cross terms (product)
+    V_BF16X3 = 64,    // ablation: only the three leading terms (~2^-17 relative)
+};
+
+// Plasticity variable a_ie: fp64, or a compensated fp32 pair (increments of
+// ~1e-6 on a ~2.5 are below fp32 half-ulp: plain fp32 would drop them).
+template <bool kPair> struct AccA;
+template <> struct AccA<false> {
+    double v;
+    __device__ void set(double x) { v = x; }
+    __device__ double get() const { return v; }
+    template <typename Real> __device__ Real val() const { return (Real)v; }
+    __device__ void add(float inc) { v += (double)inc; }
+    __device__ void add(double inc) { v += inc; }
+};
+template <> struct AccA<true> {
+    float hi, lo;
+    __device__ void set(double x) { hi = (float)x; lo = (float)(x - (double)hi); }
+    __device__ double get() const { return (double)hi + (double)lo; }
+    template <typename Real> __device__ Real val() const { return (Real)(hi + lo); }
+    __device__ void add(float inc) {  // Kahan-Babuska: |hi| >> |inc|
+        const float t = inc + lo;
+        const float s = hi + t;
+        lo = t - (s - hi);
+        hi = s;
+    }
+};
+
+template <typename Real, int NT, int NW, int VAR, int MINW>
+__global__ void __launch_bounds__(NW * 64, MINW) wc_sde_kernel(const KArgs a) {
     typedef typename Tr<Real>::acc_t acc_t;
     typedef __attribute__((ext_vector_type(4))) Real real4;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    real4* lfrag = reinterpret_cast<real4*>(smem);
+    static_assert(NT % NW == 0, "NW must divide NT");
+    constexpr int OT = NT / NW;
+    constexpr int kTerms = (VAR & V_BF16X6) ? 6 : (VAR & V_BF16X3) ? 3 : 0;
+    constexpr bool kBf = kTerms > 0;
+    static_assert(!kBf || (sizeof(Real) == 4 && NT % 2 == 0), "bf16 coupling: fp32, even tile count");
+    constexpr int NC = NT / 2;  // bf16 k-chunks (2 tiles = 32 nodes)
+    constexpr int NP = kTerms == 6 ? 3 : 2;
+    constexpr bool kFragRegs = (VAR & V_FRAG_REGS) != 0;
+    constexpr bool kRng = (VAR & V_NO_RNG) == 0;
+    constexpr bool kMfma = (VAR & V_NO_MFMA) == 0;
+    constexpr bool kPairA = sizeof(Real) == 4 && (VAR & V_KAHAN_A) != 0;
+    constexpr bool kParamRegs = sizeof(Real) == 4;  // fp64 re-reads G/sigmaE (register budget)
+    constexpr int kFragUnits = kBf ? NT * NC * 3 : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
 
-    // stage the connectome fragment image in LDS (whole workgroup)
-    {
-        const real4* gfrag = reinterpret_cast<const real4*>(a.frag);
-        for (int i = threadIdx.x; i < NT * NT * 64; i += blockDim.x) lfrag[i] = gfrag[i];
-    }
-    __syncthreads();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // LDS: [A-operand image, unless kFragRegs] [E exchange, 2 buffers, if NW > 1]
+    const size_t frag_bytes = kFragRegs ? 0 : (size_t)kFragUnits * 64 * (kBf ? 16 : sizeof(real4));
+    char* xraw = smem + frag_bytes;
+    bf16x8* xb16 = reinterpret_cast<bf16x8*>(xraw);  // [2][NC][3][64]
+    real4* xbn = reinterpret_cast<real4*>(xraw);     // [2][NT][64]
 
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int w = threadIdx.x >> 6;
     const int j = lane & 15, g = lane >> 4;
-    const int wave_sim0 = (blockIdx.x * kWaves + wave) * kSimsPerWave;
-    if (wave_sim0 >= a.B) return;  // whole wave out of range (no barrier follows)
-    const int b = wave_sim0 + j;
+    const int b = blockIdx.x * kSims + j;
     const bool live = b < a.B;
     const int bb = live ? b : a.B - 1;  // tail lanes mirror the last sim, never store
     const int N = a.N;
+    const int T0 = NW == 1 ? 0 : w * OT;
+
+    // ---- A operand: this wave's rows, in registers or the whole image in LDS ----
+    constexpr bool kRegBf = kFragRegs && kBf, kRegN = kFragRegs && !kBf;
+    bf16x8 F16[kRegBf ? OT : 1][kRegBf ? NC : 1][kRegBf ? NP : 1];
+    real4 FN[kRegN ? OT : 1][kRegN ? NT : 1];
+    {
+        const bf16x8* g16 = reinterpret_cast<const bf16x8*>(a.frag);
+        const real4* gn = reinterpret_cast<const real4*>(a.frag);
+        if constexpr (kRegBf) {
+#pragma unroll
+            for (int u = 0; u < OT; ++u)
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) F16[u][c][p] = g16[(((T0 + u) * NC + c) * 3 + p) * 64 + lane];
+        } else if constexpr (kRegN) {
+#pragma unroll
+            for (int u = 0; u < OT; ++u)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) FN[u][t] = gn[((T0 + u) * NT + t) * 64 + lane];
+        } else if constexpr (kBf) {
+            bf16x8* l16 = reinterpret_cast<bf16x8*>(smem);
+            for (int i = threadIdx.x; i < kFragUnits * 64; i += blockDim.x) l16[i] = g16[i];
+        } else {
+            real4* ln = reinterpret_cast<real4*>(smem);
+            for (int i = threadIdx.x; i < kFragUnits * 64; i += blockDim.x) ln[i] = gn[i];
+        }
+    }
 
     const uint64_t key = a.keys[bb];
-    const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
 
-    // ---- load state and per-node parameters into registers ----
-    // fp32 keeps G and sigmaE*log2(e) in registers; the fp64 parity path
-    // re-reads them (L1/L2 resident) every step to stay out of scratch
-    constexpr bool kParamRegs = sizeof(Real) == 4;
-    constexpr int PT = kParamRegs ? NT : 1;
-    Real E[NT][4], I[NT][4], Gc[PT][4], Sl[PT][4];
-    double A[NT][4];
+    // ---- own state and per-node parameters ----
+    constexpr int PT = kParamRegs ? OT : 1;
+    Real E[OT][4], I[OT][4], Gc[PT][4], Sl[PT][4];
+    AccA<kPairA> A[OT][4];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int u = 0; u < OT; ++u)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int n = 16 * t + 4 * g + r;
+            const int n = 16 * (T0 + u) + 4 * g + r;
             const bool ok = n < N;
             const size_t o = (size_t)bb * N + (ok ? n : 0);
-            E[t][r] = ok ? (Real)a.E[o] : (Real)0;
-            I[t][r] = ok ? (Real)a.I[o] : (Real)0;
-            A[t][r] = ok ? a.A[o] : 0.0;
+            E[u][r] = ok ? (Real)a.E[o] : (Real)0;
+            I[u][r] = ok ? (Real)a.I[o] : (Real)0;
+            A[u][r].set(ok ? a.A[o] : 0.0);
             if constexpr (kParamRegs) {
-                Gc[t][r] = ok ? (Real)a.G[o] : (Real)0;
-                Sl[t][r] = ok ? Tr<Real>::slope(a.sigmaE[o]) : (Real)0;
+                Gc[u][r] = ok ? (Real)a.G[o] : (Real)0;
+                Sl[u][r] = ok ? Tr<Real>::slope(a.sigmaE[o]) : (Real)0;
             }
         }
+
+    // ---- B operand (E of every node) ----
+    // NW == 1: registers.  NW > 1: each wave publishes its own tiles to the LDS
+    // image of the step, then every wave reads chunks back at the point of use
+    // (register arrays are only ever indexed by compile-time constants).
+    bf16x8 XB[(kBf && NW == 1) ? NC : 1][NP];
+    Real X[(!kBf && NW == 1) ? NT : 1][4];
+    auto publish = [&](int buf) {
+        if constexpr (NW == 1) {
+            if constexpr (kBf) {
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    bf16x4 h0, m0, l0, h1, m1, l1;
+                    split3(E[2 * c], h0, m0, l0);
+                    split3(E[2 * c + 1], h1, m1, l1);
+                    XB[c][0] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+                    XB[c][1] = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+                    if constexpr (NP == 3) XB[c][2] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) X[t][r] = E[t][r];
+            }
+        } else {
+            if constexpr (kBf) {
+                bf16x4* x4 = reinterpret_cast<bf16x4*>(xb16 + buf * NC * 3 * 64);
+#pragma unroll
+                for (int u = 0; u < OT; ++u) {
+                    const int t = T0 + u;  // chunk t/2, half t&1 (runtime: address arithmetic only)
+                    bf16x4 hmo[3];
+                    split3(E[u], hmo[0], hmo[1], hmo[2]);
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) x4[(((t >> 1) * 3 + p) * 64 + lane) * 2 + (t & 1)] = hmo[p];
+                }
+            } else {
+                real4* xb = xbn + buf * NT * 64;
+#pragma unroll
+                for (int u = 0; u < OT; ++u) xb[(T0 + u) * 64 + lane] = real4{E[u][0], E[u][1], E[u][2], E[u][3]};
+            }
+            __syncthreads();  // no LDS-DMA in flight: lgkmcnt(0) + s_barrier
+        }
+    };
+    if constexpr (!kFragRegs) __syncthreads();  // A-operand image staged
+    publish(0);
 
     const Real a_ee = (Real)a.a_ee, a_ei = (Real)a.a_ei, a_ii = (Real)a.a_ii;
     const Real P = (Real)a.P, rhoE = (Real)a.rhoE, rE = (Real)a.rE, rI = (Real)a.rI;
     const Real mu = (Real)a.mu, slI = Tr<Real>::slope(a.sigmaI), sqdtD = (Real)a.sqdtD;
     const Real dtE = (Real)(a.dtSim / a.tauE), dtI = (Real)(a.dtSim / a.tauI);
     const Real dt = (Real)a.dtSim;
-    const double dtA = a.dtSim / a.tau_ip;
-    // exact-division forms for the fp64 parity path
-    const Real tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;
+    const Real dtA = (Real)(a.dtSim / a.tau_ip);
+    const Real tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;  // fp64 exact forms
     const size_t BN = (size_t)a.B * N;
+    const int rec_every = (int)a.rec_every;
+    int rec_cnt = 0, rec_row = 0;
 
     for (int s = 0; s < a.nsteps; ++s) {
+        const int buf = s & 1;
         // ---- record the state before the update (wc:124-125) ----
-        if (a.rec_every > 0 && (s % a.rec_every) == 0) {
-            const size_t row = (size_t)(s / a.rec_every) * BN + (size_t)bb * N;
-            if (live) {
+        if (rec_every > 0) {
+            if (rec_cnt == 0) {
+                const size_t row = (size_t)rec_row * BN + (size_t)bb * N;
+                if (live) {
 #pragma unroll
-                for (int t = 0; t < NT; ++t)
+                    for (int u = 0; u < OT; ++u)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int n = 16 * t + 4 * g + r;
-                        if (n < N) {
-                            static_cast<Real*>(a.recE)[row + n] = E[t][r];
-                            if (a.recI) static_cast<Real*>(a.recI)[row + n] = I[t][r];
-                            if (a.recA) static_cast<Real*>(a.recA)[row + n] = (Real)A[t][r];
+                        for (int r = 0; r < 4; ++r) {
+                            const int n = 16 * (T0 + u) + 4 * g + r;
+                            if (n < N) {
+                                static_cast<Real*>(a.recE)[row + n] = E[u][r];
+                                if (a.recI) static_cast<Real*>(a.recI)[row + n] = I[u][r];
+                                if (a.recA) static_cast<Real*>(a.recA)[row + n] = (Real)A[u][r].get();
+                            }
                         }
+                }
+                ++rec_row;
+                rec_cnt = rec_every;
+            }
+            --rec_cnt;
+        }
+
+        // ---- coupling: acc[u][r] = sum_k CM[node(T0+u, g, r)][k] E[k]  (np.dot, wc:81) ----
+        acc_t acc[OT];
+#pragma unroll
+        for (int u = 0; u < OT; ++u) acc[u] = acc_t{0, 0, 0, 0};
+        int fl = lane;
+        if constexpr (!kFragRegs || NW > 1) asm volatile("" : "+v"(fl));  // opaque: LDS reads stay in the loop
+        if constexpr (kMfma && kBf) {
+            const bf16x8* l16 = reinterpret_cast<const bf16x8*>(smem);
+            const bf16x8* xb = xb16 + buf * NC * 3 * 64;
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                bf16x8 xe[NP];
+#pragma unroll
+                for (int p = 0; p < NP; ++p) {
+                    if constexpr (NW == 1) xe[p] = XB[c][p];
+                    else xe[p] = xb[(c * 3 + p) * 64 + fl];
+                }
+#pragma unroll
+                for (int u = 0; u < OT; ++u) {
+                    bf16x8 f[NP];
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        if constexpr (kFragRegs) f[p] = F16[u][c][p];
+                        else f[p] = l16[(((T0 + u) * NC + c) * 3 + p) * 64 + fl];
                     }
+                    // small terms first: 2^-18 (lo.hi, mid.mid, hi.lo), 2^-9 (mid.hi, hi.mid), 1 (hi.hi)
+                    if constexpr (NP == 3) {
+                        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[2], xe[0], acc[u], 0, 0, 0);
+                        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[1], xe[1], acc[u], 0, 0, 0);
+                        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[0], xe[2], acc[u], 0, 0, 0);
+                    }
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[1], xe[0], acc[u], 0, 0, 0);
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[0], xe[1], acc[u], 0, 0, 0);
+                    acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[0], xe[0], acc[u], 0, 0, 0);
+                }
+            }
+        } else if constexpr (kMfma) {
+            const real4* ln = reinterpret_cast<const real4*>(smem);
+            const real4* xb = xbn + buf * NT * 64;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                Real xe[4];
+                if constexpr (NW == 1) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xe[r] = X[t][r];
+                } else {
+                    const real4 v = xb[t * 64 + fl];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xe[r] = v[r];
+                }
+#pragma unroll
+                for (int u = 0; u < OT; ++u) {
+                    if constexpr (!kFragRegs && sizeof(Real) == 8)
+                        if ((u & 1) == 0) __builtin_amdgcn_sched_barrier(0);  // bound fp64 read look-ahead
+                    const real4 f = kFragRegs ? FN[u][t] : ln[((T0 + u) * NT + t) * 64 + fl];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[u] = Tr<Real>::mfma(f[r], xe[r], acc[u]);
+                }
             }
         }
 
-        // ---- coupling: acc[T][r] = sum_k CM[node(T,g,r)][k] * E[k]  (wc:81 np.dot) ----
-        int fl = lane;
-        if constexpr (!kHoist) asm volatile("" : "+v"(fl));  // opaque: no LICM of the LDS reads
-        acc_t acc[NT];
-#pragma unroll
-        for (int T = 0; T < NT; ++T) acc[T] = acc_t{0, 0, 0, 0};
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-            for (int T = 0; T < NT; ++T) {
-                // bound how far ahead the fp64 path issues fragment reads
-                if constexpr (!kHoist) if ((T & 1) == 0) __builtin_amdgcn_sched_barrier(0);
-                const real4 f = lfrag[(T * NT + t) * 64 + fl];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[T] = Tr<Real>::mfma(f[r], E[t][r], acc[T]);
-            }
-
         // ---- elementwise update (wc:77-83), noise drawn inside the E sigmoid ----
         const uint64_t gstep = (uint64_t)(a.step0 + s);
-        const uint32_t s_lo = (uint32_t)gstep, s_hi = (uint32_t)(gstep >> 32);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            // keep each tile's update (and its live range) in its own schedule region
-            if constexpr (sizeof(Real) == 8) __builtin_amdgcn_sched_barrier(0);
-            Real z[4];
-            quad_normals(s_lo, s_hi, (uint32_t)(4 * t + g), k0, k1, z);
+        for (int u = 0; u < OT; ++u) {
+            if constexpr (sizeof(Real) == 8) __builtin_amdgcn_sched_barrier(0);  // fp64: bound live ranges
+            Real z[4] = {0, 0, 0, 0};
+            if constexpr (kRng) quad_normals(gstep, (uint32_t)(4 * (T0 + u) + g), key, z);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const Real e = E[t][r], in = I[t][r];
-                const Real ai = (Real)A[t][r];
+                const Real e = E[u][r], in = I[u][r];
+                const Real ai = A[u][r].template val<Real>();
                 Real gc, sl;
                 if constexpr (kParamRegs) {
-                    gc = Gc[t][r];
-                    sl = Sl[t][r];
+                    gc = Gc[u][r];
+                    sl = Sl[u][r];
                 } else {
-                    const int n = 16 * t + 4 * g + r;
+                    const int n = 16 * (T0 + u) + 4 * g + r;
                     const size_t o = (size_t)bb * N + (n < N ? n : 0);
                     gc = n < N ? (Real)a.G[o] : (Real)0;
                     sl = n < N ? Tr<Real>::slope(a.sigmaE[o]) : (Real)0;
                 }
-                const Real xE = a_ee * e - ai * in + gc * acc[t][r] + P + sqdtD * z[r];
+                const Real cpl = kMfma ? acc[u][r] : e;
+                const Real xE = a_ee * e - ai * in + gc * cpl + P + sqdtD * z[r];
                 const Real SE = Tr<Real>::sig(xE, mu, sl);
                 const Real xI = a_ei * e - a_ii * in;
                 const Real SI = Tr<Real>::sig(xI, mu, slI);
@@ -284,30 +519,31 @@ __global__ void __launch_bounds__(kWaves * 64) wc_sde_kernel(const KArgs a) {
                     const Real dE = (-e + (1 - rE * e) * SE) / tauE;
                     const Real dI = (-in + (1 - rI * in) * SI) / tauI;
                     const Real dA = (in * (e - rhoE)) / tau_ip;
-                    E[t][r] = e + dt * dE;
-                    I[t][r] = in + dt * dI;
-                    A[t][r] = A[t][r] + dt * dA;
+                    E[u][r] = e + dt * dE;
+                    I[u][r] = in + dt * dI;
+                    A[u][r].add(dt * dA);
                 } else {
-                    E[t][r] = e + dtE * (-e + (1 - rE * e) * SE);
-                    I[t][r] = in + dtI * (-in + (1 - rI * in) * SI);
-                    A[t][r] = A[t][r] + dtA * (double)(in * (e - rhoE));
+                    E[u][r] = e + dtE * (-e + (1 - rE * e) * SE);
+                    I[u][r] = in + dtI * (-in + (1 - rI * in) * SI);
+                    A[u][r].add(dtA * (in * (e - rhoE)));
                 }
             }
         }
+        publish(buf ^ 1);
     }
 
-    // ---- write back the state ----
+    // ---- write back the state (own tiles) ----
     if (live) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+        for (int u = 0; u < OT; ++u)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int n = 16 * t + 4 * g + r;
+                const int n = 16 * (T0 + u) + 4 * g + r;
                 if (n < N) {
                     const size_t o = (size_t)b * N + n;
-                    a.E[o] = (double)E[t][r];
-                    a.I[o] = (double)I[t][r];
-                    a.A[o] = A[t][r];
+                    a.E[o] = (double)E[u][r];
+                    a.I[o] = (double)I[u][r];
+                    a.A[o] = A[u][r].get();
                 }
             }
     }
@@ -319,46 +555,123 @@ __global__ void noise_kernel(const uint64_t* __restrict__ keys, int B, int N, in
     const int nq = (N + 3) / 4;
     if (idx >= B * nq) return;
     const int b = idx / nq, q = idx % nq;
-    const uint64_t key = keys[b];
     Real z[4];
-    quad_normals((uint32_t)(uint64_t)step, (uint32_t)((uint64_t)step >> 32), (uint32_t)q, (uint32_t)key,
-                 (uint32_t)(key >> 32), z);
+    quad_normals((uint64_t)step, (uint32_t)q, keys[b], z);
     for (int r = 0; r < 4; ++r)
         if (4 * q + r < N) out[(size_t)b * N + 4 * q + r] = z[r];
 }
 
 int tiles_for(int N) { return (N + 15) / 16; }
 
-template <typename Real, int NT>
-int launch_nt(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
-    const int total = NT * NT * 64 * 4;
-    hipLaunchKernelGGL((build_frag<Real, NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
-                       static_cast<Real*>(ws));
-    const size_t lds = (size_t)NT * NT * 64 * 4 * sizeof(Real);
-    const int blocks = (ka.B + kSimsPerBlock - 1) / kSimsPerBlock;
-    constexpr bool hoist = sizeof(Real) == 4;
-    auto kern = wc_sde_kernel<Real, NT, hoist>;
+template <typename Real, int NT, int NW, int VAR, int MINW = 1>
+int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+    constexpr bool bf = (VAR & (V_BF16X6 | V_BF16X3)) != 0;
+    constexpr bool frag_regs = (VAR & V_FRAG_REGS) != 0;
+    size_t lds;
+    if constexpr (bf) {
+        const int total = NT * (NT / 2) * 64;
+        hipLaunchKernelGGL((build_frag_bf16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
+                           static_cast<bf16x8*>(ws));
+        lds = (frag_regs ? 0 : (size_t)NT * (NT / 2) * 3 * 64 * 16) + (NW > 1 ? (size_t)2 * (NT / 2) * 3 * 64 * 16 : 0);
+    } else {
+        const int total = NT * NT * 64 * 4;
+        hipLaunchKernelGGL((build_frag<Real, NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
+                           static_cast<Real*>(ws));
+        lds = (frag_regs ? 0 : (size_t)NT * NT * 64 * 4 * sizeof(Real)) +
+              (NW > 1 ? (size_t)2 * NT * 64 * 4 * sizeof(Real) : 0);
+    }
+    const int blocks = (ka.B + kSims - 1) / kSims;
+    auto kern = wc_sde_kernel<Real, NT, NW, VAR, MINW>;
     if (lds > 65536) {
         hipError_t ea = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (ea != hipSuccess) return set_err(WC_EHIP, hipGetErrorString(ea));
     }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), lds, st, ka);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(NW * 64), lds, st, ka);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_err(WC_EHIP, hipGetErrorString(e));
     return WC_OK;
 }
 
-template <typename Real>
-int launch(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
-    switch (tiles_for(ka.N)) {
-        case 1: return launch_nt<Real, 1>(ka, sc, ws, st);
-        case 2: return launch_nt<Real, 2>(ka, sc, ws, st);
-        case 3: return launch_nt<Real, 3>(ka, sc, ws, st);
-        case 4: return launch_nt<Real, 4>(ka, sc, ws, st);
-        case 5: return launch_nt<Real, 5>(ka, sc, ws, st);
-        case 6: return launch_nt<Real, 6>(ka, sc, ws, st);
+// ---------------- product configurations ----------------
+constexpr int kVarF32 = V_BF16X6 | V_FRAG_REGS | V_KAHAN_A;
+constexpr int kVarF64 = 0;
+
+size_t frag_bytes(int N, int precision) {
+    if (precision == WC_F64) {
+        const int nt = tiles_for(N);
+        return (size_t)nt * nt * 64 * 4 * 8;
+    }
+    const int nt = (tiles_for(N) + 1) & ~1;  // bf16 k-chunks pair tiles
+    return (size_t)nt * (nt / 2) * 3 * 64 * 16;
+}
+
+int launch_f32(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+    switch ((tiles_for(ka.N) + 1) & ~1) {
+        case 2: return launch_v<float, 2, 1, kVarF32>(ka, sc, ws, st);
+        case 4: return launch_v<float, 4, 2, kVarF32>(ka, sc, ws, st);
+        case 6: return launch_v<float, 6, 3, kVarF32>(ka, sc, ws, st);
         default: return set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
     }
+}
+
+int launch_f64(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+    switch (tiles_for(ka.N)) {
+        case 1: return launch_v<double, 1, 1, kVarF64>(ka, sc, ws, st);
+        case 2: return launch_v<double, 2, 1, kVarF64>(ka, sc, ws, st);
+        case 3: return launch_v<double, 3, 1, kVarF64>(ka, sc, ws, st);
+        case 4: return launch_v<double, 4, 1, kVarF64>(ka, sc, ws, st);
+        case 5: return launch_v<double, 5, 1, kVarF64>(ka, sc, ws, st);
+        case 6: return launch_v<double, 6, 1, kVarF64>(ka, sc, ws, st);
+        default: return set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
+    }
+}
+
+// diagnostic variants (81 <= N <= 96, fp32) for on-GPU ablation
+int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+    constexpr int K = V_KAHAN_A;
+    switch (variant) {
+        case 0: return launch_v<float, 6, 1, V_FRAG_REGS | K>(ka, sc, ws, st);          // f32 MFMA, 1 wave
+        case 1: return launch_v<float, 6, 3, V_FRAG_REGS | K>(ka, sc, ws, st);          // f32 MFMA, 3 waves
+        case 2: return launch_v<float, 6, 3, K>(ka, sc, ws, st);                        // f32 MFMA, LDS frags
+        case 3: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS | K>(ka, sc, ws, st);  // product
+        case 4: return launch_v<float, 6, 3, V_BF16X6 | K>(ka, sc, ws, st);
+        case 5: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS | K, 3>(ka, sc, ws, st);
+        case 6: return launch_v<float, 6, 3, V_BF16X6 | K, 4>(ka, sc, ws, st);
+        case 7: return launch_v<float, 6, 2, V_BF16X6 | V_FRAG_REGS | K>(ka, sc, ws, st);
+        case 8: return launch_v<float, 6, 2, V_BF16X6 | K, 3>(ka, sc, ws, st);
+        case 9: return launch_v<float, 6, 6, V_BF16X6 | K>(ka, sc, ws, st);
+        case 10: return launch_v<float, 6, 1, V_BF16X6 | V_FRAG_REGS | K>(ka, sc, ws, st);
+        case 11: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS | K | V_NO_RNG>(ka, sc, ws, st);
+        case 12: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS | K | V_NO_MFMA>(ka, sc, ws, st);
+        case 13: return launch_v<float, 6, 3, V_BF16X3 | V_FRAG_REGS | K>(ka, sc, ws, st);
+        case 14: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS>(ka, sc, ws, st);  // fp64 a_ie
+        default: return set_err(WC_EINVAL, "unknown diagnostic variant");
+    }
+}
+
+int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
+              const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
+              int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* recI, void* recA,
+              void* workspace, size_t ws_bytes) {
+    g_err[0] = 0;
+    if (!p || B <= 0 || N <= 0 || nsteps < 0 || nsteps > INT32_MAX || step0 < 0 || rec_every < 0 ||
+        rec_every > INT32_MAX || step0 + nsteps > (int64_t(1) << 48))
+        return set_err(WC_EINVAL, "wc_integrate: invalid B/N/nsteps/step0/rec_every");
+    if (!sc || !G || !sigmaE || !keys || !E || !I || !A)
+        return set_err(WC_EINVAL, "wc_integrate: NULL array argument");
+    if (precision != WC_F32 && precision != WC_F64) return set_err(WC_EINVAL, "wc_integrate: bad precision");
+    if (rec_every > 0 && !recE) return set_err(WC_EINVAL, "wc_integrate: rec_every > 0 needs recE");
+    if (tiles_for(N) > kMaxTiles) return set_err(WC_EUNSUPPORTED, "wc_integrate: N > 96 not supported");
+    if (!workspace || ws_bytes < frag_bytes(N, precision))
+        return set_err(WC_EWORKSPACE, "wc_integrate: workspace too small");
+    ka.a_ee = p->a_ee; ka.a_ei = p->a_ei; ka.a_ii = p->a_ii;
+    ka.tauE = p->tauE; ka.tauI = p->tauI; ka.P = p->P; ka.rhoE = p->rhoE;
+    ka.rE = p->rE; ka.rI = p->rI; ka.mu = p->mu; ka.sigmaI = p->sigmaI;
+    ka.sqdtD = p->sqdtD; ka.dtSim = p->dtSim; ka.tau_ip = tau_ip;
+    ka.G = G; ka.sigmaE = sigmaE; ka.keys = keys; ka.E = E; ka.I = I; ka.A = A;
+    ka.frag = workspace; ka.recE = recE; ka.recI = recI; ka.recA = recA;
+    ka.step0 = step0; ka.rec_every = rec_every; ka.nsteps = (int)nsteps; ka.B = B; ka.N = N;
+    return WC_OK;
 }
 
 }  // namespace
@@ -371,40 +684,42 @@ const char* wc_last_error(void) { return g_err; }
 
 size_t wc_workspace_size(int N, int precision) {
     if (N <= 0) return 0;
+    // the diagnostic f32-MFMA variants need the native image; size for the larger
     const int nt = tiles_for(N);
-    return (size_t)nt * nt * 64 * 4 * (precision == WC_F64 ? 8 : 4);
+    const size_t native = (size_t)nt * nt * 64 * 4 * (precision == WC_F64 ? 8 : 4);
+    const size_t need = frag_bytes(N, precision);
+    return need > native ? need : native;
 }
 
 int wc_integrate(const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
-                 const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A,
-                 int64_t step0, int64_t nsteps, double tau_ip, int64_t rec_every, void* recE,
-                 void* recI, void* recA, void* workspace, size_t ws_bytes, void* stream) {
-    g_err[0] = 0;
-    if (!p || B <= 0 || N <= 0 || nsteps < 0 || nsteps > INT32_MAX || step0 < 0 || rec_every < 0)
-        return set_err(WC_EINVAL, "wc_integrate: invalid B/N/nsteps/step0/rec_every");
-    if (!sc || !G || !sigmaE || !keys || !E || !I || !A)
-        return set_err(WC_EINVAL, "wc_integrate: NULL array argument");
-    if (precision != WC_F32 && precision != WC_F64) return set_err(WC_EINVAL, "wc_integrate: bad precision");
-    if (rec_every > 0 && !recE) return set_err(WC_EINVAL, "wc_integrate: rec_every > 0 needs recE");
-    if (tiles_for(N) > kMaxTiles) return set_err(WC_EUNSUPPORTED, "wc_integrate: N > 96 not supported");
-    if (!workspace || ws_bytes < wc_workspace_size(N, precision))
-        return set_err(WC_EWORKSPACE, "wc_integrate: workspace too small");
-    if (nsteps == 0) return WC_OK;
+                 const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
+                 int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* recI, void* recA,
+                 void* workspace, size_t ws_bytes, void* stream) {
     KArgs ka;
-    ka.a_ee = p->a_ee; ka.a_ei = p->a_ei; ka.a_ii = p->a_ii;
-    ka.tauE = p->tauE; ka.tauI = p->tauI; ka.P = p->P; ka.rhoE = p->rhoE;
-    ka.rE = p->rE; ka.rI = p->rI; ka.mu = p->mu; ka.sigmaI = p->sigmaI;
-    ka.sqdtD = p->sqdtD; ka.dtSim = p->dtSim; ka.tau_ip = tau_ip;
-    ka.G = G; ka.sigmaE = sigmaE; ka.keys = keys; ka.E = E; ka.I = I; ka.A = A;
-    ka.frag = workspace; ka.recE = recE; ka.recI = recI; ka.recA = recA;
-    ka.step0 = step0; ka.rec_every = rec_every; ka.nsteps = (int)nsteps; ka.B = B; ka.N = N;
+    int rc = make_args(ka, p, precision, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, recE,
+                       recI, recA, workspace, ws_bytes);
+    if (rc != WC_OK || nsteps == 0) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    return precision == WC_F64 ? launch<double>(ka, sc, workspace, st) : launch<float>(ka, sc, workspace, st);
+    return precision == WC_F64 ? launch_f64(ka, sc, workspace, st) : launch_f32(ka, sc, workspace, st);
+}
+
+int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const double* sc, const double* G,
+                      const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
+                      int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* workspace,
+                      size_t ws_bytes, void* stream) {
+    KArgs ka;
+    int rc = make_args(ka, p, WC_F32, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, recE,
+                       nullptr, nullptr, workspace, ws_bytes);
+    if (rc != WC_OK || nsteps == 0) return rc;
+    if (tiles_for(N) != 6) return set_err(WC_EUNSUPPORTED, "wc_diag_integrate: needs 81 <= N <= 96");
+    if (ws_bytes < wc_workspace_size(N, WC_F32)) return set_err(WC_EWORKSPACE, "wc_diag_integrate: workspace");
+    return launch_diag(variant, ka, sc, workspace, static_cast<hipStream_t>(stream));
 }
 
 int wc_noise(int precision, int B, int N, const uint64_t* keys, int64_t step, void* out, void* stream) {
     g_err[0] = 0;
-    if (B <= 0 || N <= 0 || !keys || !out || step < 0) return set_err(WC_EINVAL, "wc_noise: bad arguments");
+    if (B <= 0 || N <= 0 || !keys || !out || step < 0 || step >= (int64_t(1) << 48) || N > 4 * 65536)
+        return set_err(WC_EINVAL, "wc_noise: bad arguments");
     const int nq = (N + 3) / 4;
     const int total = B * nq;
     hipStream_t st = static_cast<hipStream_t>(stream);

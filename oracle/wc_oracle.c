@@ -14,8 +14,10 @@
  * SURVEY.md 8c) replaced by the build's deterministic noise stream:
  *
  *   Philox4x32-10 (Salmon et al., SC'11 "Parallel random numbers: as easy as
- *   1, 2, 3"; Random123 constants), key = per-simulation 64-bit key,
- *   counter = (global Euler step lo32, hi32, node quad q = node/4, 0).
+ *   1, 2, 3"; Random123 constants) with the fixed key (WC_PHILOX_KEY0/1 of
+ *   include/wcsde.h) and counter = (step lo32, (step hi16 << 16) | quad,
+ *   simkey lo32, simkey hi32) for global Euler step `step`, node quad
+ *   q = node/4 and the 64-bit per-simulation key.
  *   The four 32-bit outputs feed two Box-Muller pairs:
  *     u = (2*(x >> 9) + 1) * 2^-24           (exact in fp32 and fp64, in (0,1))
  *     z0 = sqrt(-2 ln u1) cos(2 pi u2),  z1 = sqrt(-2 ln u1) sin(2 pi u2)
@@ -77,8 +79,9 @@ static const double TWO_PI = 6.283185307179586476925286766559;
 /* standard normals of the 4 nodes of quad q at global step `step` */
 static inline void quad_normals(uint64_t key, int64_t step, uint32_t q, double z[4])
 {
-    uint32_t ctr[4] = {(uint32_t)(uint64_t)step, (uint32_t)((uint64_t)step >> 32), q, 0u};
-    uint32_t k[2] = {(uint32_t)key, (uint32_t)(key >> 32)};
+    const uint64_t st = (uint64_t)step;
+    uint32_t ctr[4] = {(uint32_t)st, ((uint32_t)(st >> 32) << 16) | q, (uint32_t)key, (uint32_t)(key >> 32)};
+    uint32_t k[2] = {0x243F6A88u, 0x85A308D3u};  /* WC_PHILOX_KEY0/1 */
     uint32_t x[4];
     orc_philox4x32_10(ctr, k, x);
     double r0 = sqrt(-2.0 * log(u01(x[0])));

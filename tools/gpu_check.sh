@@ -1,0 +1,30 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, short bench, rocprof kernel trace.
+# Stops at the first crash/timeout (exit codes other than 0/1 from pytest).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+STEPS="${STEPS:-tests smoke bench prof}"
+fatal() { local rc=$1; [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; }
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -q -rA > $OUT/pytest_gpu.log 2>&1; rc=$?
+      echo "pytest gpu rc=$rc"; tail -25 $OUT/pytest_gpu.log
+      if fatal $rc; then echo "STOP after tests"; exit $rc; fi ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
+      echo "smoke rc=$rc"; tail -5 $OUT/smoke.log
+      if [ $rc -ne 0 ]; then echo "STOP after smoke"; exit $rc; fi ;;
+    bench)
+      timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1; rc=$?
+      echo "bench rc=$rc"; tail -5 $OUT/bench.log
+      if [ $rc -ne 0 ]; then echo "STOP after bench"; exit $rc; fi ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o sde -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1; rc=$?
+      echo "prof rc=$rc"; tail -3 $OUT/prof.log; find $OUT/prof -name "*stats*" | head
+      if [ $rc -ne 0 ]; then echo "STOP after prof"; exit $rc; fi ;;
+  esac
+done
