@@ -85,9 +85,12 @@ size_t wc_workspace_size(int N, int precision);
  *  E,I,A     [B][N] fp64     state (E, I, a_ie), read at entry, written at exit
  *  step0                     global step index of the first step (Philox counter)
  *  rec_every >0: store the state BEFORE the update of every local step s with
- *            s % rec_every == 0 (wc:124-125) at row s/rec_every of recE/recI/recA,
- *            layout [n_rec][B][N], element type float (WC_F32) or double (WC_F64);
+ *            s % rec_every == 0 (wc:124-125) as record k = s/rec_every in
+ *            recE/recI/recA, element type float (WC_F32) or double (WC_F64);
  *            recI/recA may be NULL.  rec_every == 0: no recording.
+ *  rec_ld    0: records time-major [n_rec][B][N] (Y_t[:, k, :] of run());
+ *            > 0: node-major, record k of column c = b*N + n at c*rec_ld + k
+ *            (a slot of the sweep pipeline's E ring, read by BOLD and Welch).
  *  precision WC_F32: E, I, sigmoids in fp32; coupling as six bf16 MFMA cross
  *            terms of 3-way split operands with fp32 accumulation (fp32-
  *            equivalent); a_ie as a compensated fp32 pair;
@@ -97,13 +100,73 @@ int wc_integrate(const wc_params* p, int precision, int B, int N,
                  const double* sc, const double* G, const double* sigmaE,
                  const uint64_t* keys, double* E, double* I, double* A,
                  int64_t step0, int64_t nsteps, double tau_ip,
-                 int64_t rec_every, void* recE, void* recI, void* recA,
+                 int64_t rec_every, int64_t rec_ld, void* recE, void* recI, void* recA,
                  void* workspace, size_t ws_bytes, void* stream);
 
 /* Standard normals the integrator draws at global step `step`: out [B][N]
  * (float or double per precision).  Test hook for the noise stream. */
 int wc_noise(int precision, int B, int N, const uint64_t* keys, int64_t step,
              void* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * simBOLD (netwWilsonCowanPlastic.py:140-158), streamed.
+ * Columns c = b*N + n.  The caller allocates wc_bold_state_doubles() doubles
+ * of device state, calls wc_bold_init once, wc_bold_chunk for consecutive
+ * sample ranges [t0, t0+Tc) of the E trajectory (any chunking), and
+ * wc_bold_finish once every sample 0..n_total-1 has been fed: out [M][C] is
+ * filtfilt(b, a, BOLD[neq:], axis=0)[::dec], M = ceil((n_total-neq)/dec).
+ * BOLD = Balloon-Windkessel of E at step dt (assumed form of the missing
+ * BOLDModel.BD.Sim). */
+typedef struct wc_bold_cfg {
+    double dt;        /* BOLD Euler step: dt*downsamp = 0.04 (wc:144, wc:148) */
+    int64_t neq;      /* leading samples dropped (Neq = 2000, wc:145) */
+    int64_t n_total;  /* samples of E_t (len(wc.time) = 300000) */
+    int64_t dec;      /* BOLD_downsamp (1000; cortex_run.py uses 10) */
+    double b[5], a[5]; /* band-pass, a[0] = 1: bessel(2, [2*.01*dt, 2*.1*dt], 'bandpass') (wc:152) */
+    double zi[4];     /* scipy.signal.lfilter_zi(b, a) */
+} wc_bold_cfg;
+
+int64_t wc_bold_blocks(const wc_bold_cfg* cfg);
+size_t wc_bold_state_doubles(const wc_bold_cfg* cfg, int64_t C);
+int wc_bold_init(const wc_bold_cfg* cfg, int64_t C, double* state, void* stream);
+/* E: float (e_f64 = 0) or double; e_ld == 0: time-major [Tc][C]; e_ld > 0:
+ * node-major, sample tt of column c at E[c*e_ld + tt]. */
+int wc_bold_chunk(const wc_bold_cfg* cfg, int64_t C, const void* E, int e_f64, int64_t e_ld,
+                  int64_t t0, int64_t Tc, double* state, void* stream);
+int wc_bold_finish(const wc_bold_cfg* cfg, int64_t C, const double* state, double* out, void* stream);
+
+/* Unit phasors exp(i angle(hilbert(x, axis=0))) of every column of x [M][C]
+ * (utils.kuramoto, utils.py:35-37): phasor [M][C][2] (cos, sin).  workspace:
+ * >= M doubles. */
+int wc_hilbert_phase(int64_t C, int M, const double* x, double* phasor, void* workspace,
+                     size_t ws_bytes, void* stream);
+
+/* Per simulation b of bold [M][B][N] (the filtered, decimated BOLD; or, with
+ * bold == NULL, of the given fc_in [B][N][N]):
+ *   fc_out [B][N][N]  np.corrcoef(BOLD.T)                (may be NULL)
+ *   metrics [B][K][4] utils.get_all_metrics(sFC, empfc[k], 1) = corr, euc, ssim, new_metric
+ *   extra [B][3]      np.mean(sFC), kuramoto sync, meta (sync/meta 0 if phasor NULL)
+ * 7 <= N <= 96. */
+int wc_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, const double* empfc,
+                  int K, const double* phasor, double* fc_out, double* metrics, double* extra,
+                  void* stream);
+
+/* ------------------------------------------------------------------------
+ * Welch peak frequency (whole_sweep_both.py:90-95): signal.welch(E_t.T, fs,
+ * nperseg=4000), node-mean PSD, first argmax.  wc_welch_prepare fills the
+ * twiddle workspace once; wc_welch_accumulate adds one segment
+ * [seg0, seg0+4000) of every column to acc [B][2001] (fp64, zero it first);
+ * E is node-major: sample t of column c at
+ *   c*ld + ((t / slot) % nslots) * slot + t % slot   (a ring of nslots slots);
+ * wc_welch_peak turns acc (nseg segments) into peak [B] (Hz) and optionally
+ * the node-mean density PSD psd [B][2001]. */
+size_t wc_welch_workspace_size(void);
+int wc_welch_bins(void);
+int wc_welch_prepare(void* workspace, size_t ws_bytes, void* stream);
+int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int64_t slot,
+                        int64_t nslots, int64_t seg0, const void* workspace, double* acc, void* stream);
+int wc_welch_peak(int B, int N, int nseg, double fs, const double* acc, double* peak, double* psd,
+                  void* stream);
 
 /* Diagnostic: wc_integrate (WC_F32, no recI/recA) through compile-time kernel
  * variant `variant` (ablations / alternative tilings, see wc_sde.hip

@@ -23,6 +23,13 @@ class WCParamsC(ctypes.Structure):
         "sqdtD", "dtSim")]
 
 
+class WCBoldCfgC(ctypes.Structure):
+    """Mirror of ``wc_bold_cfg`` (include/wcsde.h)."""
+    _fields_ = [("dt", ctypes.c_double), ("neq", ctypes.c_int64), ("n_total", ctypes.c_int64),
+                ("dec", ctypes.c_int64), ("b", ctypes.c_double * 5), ("a", ctypes.c_double * 5),
+                ("zi", ctypes.c_double * 4)]
+
+
 class WCSDEError(RuntimeError):
     pass
 
@@ -37,8 +44,22 @@ _SIGNATURES = {
     "wc_workspace_size": (c_sz, [c_int, c_int]),
     "wc_integrate": (c_int, [ctypes.POINTER(WCParamsC), c_int, c_int, c_int,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                             c_i64, c_i64, c_dbl, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+                             c_i64, c_i64, c_dbl, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "wc_noise": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_vp]),
+    "wc_diag_integrate": (c_int, [c_int, ctypes.POINTER(WCParamsC), c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp, c_vp, c_vp, c_i64, c_i64, c_dbl, c_i64, c_vp, c_vp, c_sz, c_vp]),
+    "wc_bold_blocks": (c_i64, [ctypes.POINTER(WCBoldCfgC)]),
+    "wc_bold_state_doubles": (c_sz, [ctypes.POINTER(WCBoldCfgC), c_i64]),
+    "wc_bold_init": (c_int, [ctypes.POINTER(WCBoldCfgC), c_i64, c_vp, c_vp]),
+    "wc_bold_chunk": (c_int, [ctypes.POINTER(WCBoldCfgC), c_i64, c_vp, c_int, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "wc_bold_finish": (c_int, [ctypes.POINTER(WCBoldCfgC), c_i64, c_vp, c_vp, c_vp]),
+    "wc_hilbert_phase": (c_int, [c_i64, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "wc_fc_metrics": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wc_welch_workspace_size": (c_sz, []),
+    "wc_welch_bins": (c_int, []),
+    "wc_welch_prepare": (c_int, [c_vp, c_sz, c_vp]),
+    "wc_welch_accumulate": (c_int, [c_int, c_int, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "wc_welch_peak": (c_int, [c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp]),
 }
 
 

@@ -26,15 +26,10 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
-#include "../../include/wcsde.h"
+#include "wc_common.h"
 
 namespace {
 
-thread_local char g_err[512];
-int set_err(int code, const char* msg) {
-    snprintf(g_err, sizeof g_err, "%s", msg);
-    return code;
-}
 
 constexpr int kSims = 16;     // simulations per workgroup (MFMA N dimension)
 constexpr int kMaxTiles = 6;  // N <= 96 on the register-resident path
@@ -168,6 +163,7 @@ struct KArgs {
     void* recA;
     int64_t step0;
     int64_t rec_every;
+    int64_t rec_ld;  // 0: records [n_rec][B][N]; >0: node-major, (k, c) at c*rec_ld + k
     int nsteps;
     int B, N;
 };
@@ -408,7 +404,6 @@ __global__ void __launch_bounds__(NW * 64, MINW) wc_sde_kernel(const KArgs a) {
         // ---- record the state before the update (wc:124-125) ----
         if (rec_every > 0) {
             if (rec_cnt == 0) {
-                const size_t row = (size_t)rec_row * BN + (size_t)bb * N;
                 if (live) {
 #pragma unroll
                     for (int u = 0; u < OT; ++u)
@@ -416,9 +411,11 @@ __global__ void __launch_bounds__(NW * 64, MINW) wc_sde_kernel(const KArgs a) {
                         for (int r = 0; r < 4; ++r) {
                             const int n = 16 * (T0 + u) + 4 * g + r;
                             if (n < N) {
-                                static_cast<Real*>(a.recE)[row + n] = E[u][r];
-                                if (a.recI) static_cast<Real*>(a.recI)[row + n] = I[u][r];
-                                if (a.recA) static_cast<Real*>(a.recA)[row + n] = (Real)A[u][r].get();
+                                const size_t cc = (size_t)bb * N + n;
+                                const size_t o = a.rec_ld ? cc * a.rec_ld + rec_row : (size_t)rec_row * BN + cc;
+                                static_cast<Real*>(a.recE)[o] = E[u][r];
+                                if (a.recI) static_cast<Real*>(a.recI)[o] = I[u][r];
+                                if (a.recA) static_cast<Real*>(a.recA)[o] = (Real)A[u][r].get();
                             }
                         }
                 }
@@ -584,11 +581,11 @@ int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     auto kern = wc_sde_kernel<Real, NT, NW, VAR, MINW>;
     if (lds > 65536) {
         hipError_t ea = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (ea != hipSuccess) return set_err(WC_EHIP, hipGetErrorString(ea));
+        if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
     }
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(NW * 64), lds, st, ka);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return set_err(WC_EHIP, hipGetErrorString(e));
+    if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
     return WC_OK;
 }
 
@@ -610,7 +607,7 @@ int launch_f32(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
         case 2: return launch_v<float, 2, 1, kVarF32>(ka, sc, ws, st);
         case 4: return launch_v<float, 4, 2, kVarF32>(ka, sc, ws, st);
         case 6: return launch_v<float, 6, 3, kVarF32>(ka, sc, ws, st);
-        default: return set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
+        default: return wc_set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
     }
 }
 
@@ -622,7 +619,7 @@ int launch_f64(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
         case 4: return launch_v<double, 4, 1, kVarF64>(ka, sc, ws, st);
         case 5: return launch_v<double, 5, 1, kVarF64>(ka, sc, ws, st);
         case 6: return launch_v<double, 6, 1, kVarF64>(ka, sc, ws, st);
-        default: return set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
+        default: return wc_set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
     }
 }
 
@@ -645,32 +642,33 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 12: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS | K | V_NO_MFMA>(ka, sc, ws, st);
         case 13: return launch_v<float, 6, 3, V_BF16X3 | V_FRAG_REGS | K>(ka, sc, ws, st);
         case 14: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS>(ka, sc, ws, st);  // fp64 a_ie
-        default: return set_err(WC_EINVAL, "unknown diagnostic variant");
+        default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
 
 int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
               const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
-              int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* recI, void* recA,
-              void* workspace, size_t ws_bytes) {
-    g_err[0] = 0;
+              int64_t nsteps, double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI,
+              void* recA, void* workspace, size_t ws_bytes) {
+    wc_clear_err();
     if (!p || B <= 0 || N <= 0 || nsteps < 0 || nsteps > INT32_MAX || step0 < 0 || rec_every < 0 ||
-        rec_every > INT32_MAX || step0 + nsteps > (int64_t(1) << 48))
-        return set_err(WC_EINVAL, "wc_integrate: invalid B/N/nsteps/step0/rec_every");
+        rec_every > INT32_MAX || step0 + nsteps > (int64_t(1) << 48) || rec_ld < 0 ||
+        (rec_every > 0 && rec_ld > 0 && rec_ld < (nsteps + rec_every - 1) / rec_every))
+        return wc_set_err(WC_EINVAL, "wc_integrate: invalid B/N/nsteps/step0/rec_every");
     if (!sc || !G || !sigmaE || !keys || !E || !I || !A)
-        return set_err(WC_EINVAL, "wc_integrate: NULL array argument");
-    if (precision != WC_F32 && precision != WC_F64) return set_err(WC_EINVAL, "wc_integrate: bad precision");
-    if (rec_every > 0 && !recE) return set_err(WC_EINVAL, "wc_integrate: rec_every > 0 needs recE");
-    if (tiles_for(N) > kMaxTiles) return set_err(WC_EUNSUPPORTED, "wc_integrate: N > 96 not supported");
+        return wc_set_err(WC_EINVAL, "wc_integrate: NULL array argument");
+    if (precision != WC_F32 && precision != WC_F64) return wc_set_err(WC_EINVAL, "wc_integrate: bad precision");
+    if (rec_every > 0 && !recE) return wc_set_err(WC_EINVAL, "wc_integrate: rec_every > 0 needs recE");
+    if (tiles_for(N) > kMaxTiles) return wc_set_err(WC_EUNSUPPORTED, "wc_integrate: N > 96 not supported");
     if (!workspace || ws_bytes < frag_bytes(N, precision))
-        return set_err(WC_EWORKSPACE, "wc_integrate: workspace too small");
+        return wc_set_err(WC_EWORKSPACE, "wc_integrate: workspace too small");
     ka.a_ee = p->a_ee; ka.a_ei = p->a_ei; ka.a_ii = p->a_ii;
     ka.tauE = p->tauE; ka.tauI = p->tauI; ka.P = p->P; ka.rhoE = p->rhoE;
     ka.rE = p->rE; ka.rI = p->rI; ka.mu = p->mu; ka.sigmaI = p->sigmaI;
     ka.sqdtD = p->sqdtD; ka.dtSim = p->dtSim; ka.tau_ip = tau_ip;
     ka.G = G; ka.sigmaE = sigmaE; ka.keys = keys; ka.E = E; ka.I = I; ka.A = A;
     ka.frag = workspace; ka.recE = recE; ka.recI = recI; ka.recA = recA;
-    ka.step0 = step0; ka.rec_every = rec_every; ka.nsteps = (int)nsteps; ka.B = B; ka.N = N;
+    ka.step0 = step0; ka.rec_every = rec_every; ka.rec_ld = rec_ld; ka.nsteps = (int)nsteps; ka.B = B; ka.N = N;
     return WC_OK;
 }
 
@@ -680,7 +678,7 @@ extern "C" {
 
 int wcsde_abi_version(void) { return WCSDE_ABI_VERSION; }
 
-const char* wc_last_error(void) { return g_err; }
+const char* wc_last_error(void) { return wc_errbuf(); }
 
 size_t wc_workspace_size(int N, int precision) {
     if (N <= 0) return 0;
@@ -693,11 +691,11 @@ size_t wc_workspace_size(int N, int precision) {
 
 int wc_integrate(const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
                  const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
-                 int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* recI, void* recA,
-                 void* workspace, size_t ws_bytes, void* stream) {
+                 int64_t nsteps, double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI,
+                 void* recA, void* workspace, size_t ws_bytes, void* stream) {
     KArgs ka;
-    int rc = make_args(ka, p, precision, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, recE,
-                       recI, recA, workspace, ws_bytes);
+    int rc = make_args(ka, p, precision, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld,
+                       recE, recI, recA, workspace, ws_bytes);
     if (rc != WC_OK || nsteps == 0) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     return precision == WC_F64 ? launch_f64(ka, sc, workspace, st) : launch_f32(ka, sc, workspace, st);
@@ -708,18 +706,18 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
                       int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* workspace,
                       size_t ws_bytes, void* stream) {
     KArgs ka;
-    int rc = make_args(ka, p, WC_F32, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, recE,
-                       nullptr, nullptr, workspace, ws_bytes);
+    int rc = make_args(ka, p, WC_F32, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, 0,
+                       recE, nullptr, nullptr, workspace, ws_bytes);
     if (rc != WC_OK || nsteps == 0) return rc;
-    if (tiles_for(N) != 6) return set_err(WC_EUNSUPPORTED, "wc_diag_integrate: needs 81 <= N <= 96");
-    if (ws_bytes < wc_workspace_size(N, WC_F32)) return set_err(WC_EWORKSPACE, "wc_diag_integrate: workspace");
+    if (tiles_for(N) != 6) return wc_set_err(WC_EUNSUPPORTED, "wc_diag_integrate: needs 81 <= N <= 96");
+    if (ws_bytes < wc_workspace_size(N, WC_F32)) return wc_set_err(WC_EWORKSPACE, "wc_diag_integrate: workspace");
     return launch_diag(variant, ka, sc, workspace, static_cast<hipStream_t>(stream));
 }
 
 int wc_noise(int precision, int B, int N, const uint64_t* keys, int64_t step, void* out, void* stream) {
-    g_err[0] = 0;
+    wc_clear_err();
     if (B <= 0 || N <= 0 || !keys || !out || step < 0 || step >= (int64_t(1) << 48) || N > 4 * 65536)
-        return set_err(WC_EINVAL, "wc_noise: bad arguments");
+        return wc_set_err(WC_EINVAL, "wc_noise: bad arguments");
     const int nq = (N + 3) / 4;
     const int total = B * nq;
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -730,7 +728,7 @@ int wc_noise(int precision, int B, int N, const uint64_t* keys, int64_t step, vo
         hipLaunchKernelGGL(noise_kernel<float>, dim3((total + 255) / 256), dim3(256), 0, st, keys, B, N, step,
                            static_cast<float*>(out));
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return set_err(WC_EHIP, hipGetErrorString(e));
+    if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
     return WC_OK;
 }
 

@@ -1,0 +1,748 @@
+// wc_signal.hip -- the per-simulation signal chain after the integrator, on gfx950.
+//
+// Replaces, for a whole batch of simulations at once:
+//   simBOLD  (netwWilsonCowanPlastic.py:140-158): BD.Sim -> drop Neq -> Bessel
+//            band-pass filtfilt (axis 0) -> [::BOLD_downsamp]
+//   sFC = np.corrcoef(BOLD.T)                   (whole_sweep_both.py:81)
+//   utils.get_all_metrics(sFC, empFC, 1) x K    (utils.py:42-50, whole_sweep_both.py:83-86)
+//   utils.kuramoto(BOLD), np.mean(sFC)          (utils.py:34-40, whole_sweep_both.py:93-94)
+//
+// Columns: one (simulation, node) time series = column c = b*N + n; every
+// trajectory array is time-major [t][C] so consecutive threads read
+// consecutive addresses at every time step (HBM-coalesced).
+//
+// filtfilt without the trajectory (DESIGN.md "Kernel 2"): the forward IIR is
+// causal and streams with the BOLD ODE.  The backward IIR is linear, so over a
+// decimation block of L samples its state obeys z_out = A^L z_in + u and the
+// decimated output is y_zs + c A^(L-1) z_in, where (y_zs, u) come from a zero-
+// state backward pass over the block alone.  wc_bold_chunk keeps one block of
+// forward output per column and emits (y_zs, u); wc_bold_finish runs the
+// 298-step backward recursion over blocks from the end state of the
+// odd-extended tail -- exactly filtfilt's result, never holding more than one
+// block of samples.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <algorithm>
+#include <complex>
+#include <cstdlib>
+#include "wc_common.h"
+
+namespace {
+
+
+constexpr int kPad = 15;  // filtfilt padlen = 3*max(len(a), len(b)) for an order-4 filter
+
+// state layout (doubles), all [k][C] planes
+struct BoldLayout {
+    int64_t C, M;
+    int64_t bal, zf, head, x16, ring, yzs, u, zend, total;
+    __host__ __device__ BoldLayout(int64_t C_, int64_t M_, int64_t dec) : C(C_), M(M_) {
+        bal = 0;                 // 4: s, f, v, q
+        zf = bal + 4 * C;        // 4: forward IIR state
+        head = zf + 4 * C;       // 16: x[0..15]
+        x16 = head + 16 * C;     // 16: x[n-16..n-1]
+        ring = x16 + 16 * C;     // dec: forward output of the current block
+        yzs = ring + dec * C;    // M: zero-state backward output at each block start
+        u = yzs + M * C;         // 4M: zero-state backward state after each block
+        zend = u + 4 * M * C;    // 4: backward state entering the last sample
+        total = zend + 4 * C;
+    }
+};
+
+// scipy lfilter (DF2T) in scipy's association order; no fma contraction so the
+// rounding matches the reference path as closely as the hardware allows
+#pragma clang fp contract(off)
+__device__ __forceinline__ double iir_step(double z[4], double x, const double* b, const double* a) {
+    const double y = z[0] + x * b[0];
+    z[0] = z[1] + x * b[1] - y * a[1];
+    z[1] = z[2] + x * b[2] - y * a[2];
+    z[2] = z[3] + x * b[3] - y * a[3];
+    z[3] = x * b[4] - y * a[4];
+    return y;
+}
+#pragma clang fp contract(on)
+
+struct BoldArgs {
+    wc_bold_cfg cfg;
+    int64_t C, n, M;
+    double itaus, itauf, itauo, ialpha, Eo, vo, k1, k2, k3, log1mEo;
+};
+
+// zero-state backward pass over one block of forward output held in the ring
+__device__ __forceinline__ void process_block(const BoldArgs& a, const BoldLayout& L, double* st, int64_t c,
+                                              int64_t m, int64_t len) {
+    double z[4] = {0, 0, 0, 0};
+    double yzs = 0;
+    for (int64_t kk = len - 1; kk >= 0; --kk) {
+        const double y = st[L.ring + kk * L.C + c];
+        yzs = iir_step(z, y, a.cfg.b, a.cfg.a);
+    }
+    st[L.yzs + m * L.C + c] = yzs;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st[L.u + (m * 4 + k) * L.C + c] = z[k];
+}
+
+__device__ __forceinline__ void emit(const BoldArgs& a, const BoldLayout& L, double* st, int64_t c, int64_t k,
+                                     double y) {
+    const int64_t dec = a.cfg.dec;
+    const int64_t r = k % dec;
+    st[L.ring + r * L.C + c] = y;
+    if (r == dec - 1 || k == a.n - 1) process_block(a, L, st, c, k / dec, r + 1);
+}
+
+// E layout: e_ld == 0 -> time-major [Tc][C]; e_ld > 0 -> node-major, sample tt of
+// column c at c*e_ld + tt (a slot of the integrator's recording ring)
+template <typename ET>
+__global__ void bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, int64_t e_ld, int64_t t0, int64_t Tc,
+                                  double* __restrict__ st) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.C) return;
+    const BoldLayout L(a.C, a.M, a.cfg.dec);
+    const double* b = a.cfg.b;
+    const double* fa = a.cfg.a;
+    double s = st[L.bal + c], f = st[L.bal + a.C + c], v = st[L.bal + 2 * a.C + c], q = st[L.bal + 3 * a.C + c];
+    double zf[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) zf[k] = st[L.zf + k * a.C + c];
+    const int64_t neq = a.cfg.neq, n = a.n;
+    const double dt = a.cfg.dt;
+    for (int64_t tt = 0; tt < Tc; ++tt) {
+        const int64_t t = t0 + tt;
+        // Balloon-Windkessel: BOLD[t] from the state after t steps (see oracle/wc_oracle.c orc_bold)
+        const double bold = a.vo * (a.k1 * (1.0 - q) + a.k2 * (1.0 - q / v) + a.k3 * (1.0 - v));
+        const double x = (double)E[e_ld ? c * e_ld + tt : tt * a.C + c];
+        const double vpow = exp(log(v) * a.ialpha);
+        const double fpow = exp(a.log1mEo / f);
+        const double ds = x - a.itaus * s - a.itauf * (f - 1.0);
+        const double dv = (f - vpow) * a.itauo;
+        const double dq = (f * (1.0 - fpow) / a.Eo - q * vpow / v) * a.itauo;
+        const double df = s;
+        s += dt * ds;
+        f += dt * df;
+        v += dt * dv;
+        q += dt * dq;
+        if (t < neq) continue;
+        const int64_t i = t - neq;  // data index of this BOLD sample
+        if (i >= n) continue;
+        if (i >= n - 16) st[L.x16 + (i - (n - 16)) * a.C + c] = bold;
+        if (i < 16) st[L.head + i * a.C + c] = bold;
+        if (i < kPad) continue;
+        if (i == kPad) {
+            // odd extension in front: ext = 2 x0 - x[15..1], then x[0..15]; zi * ext[0]
+            const double x0 = st[L.head + c];
+            const double e0 = 2.0 * x0 - st[L.head + 15 * a.C + c];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) zf[k] = a.cfg.zi[k] * e0;
+            for (int k = 15; k >= 1; --k) iir_step(zf, 2.0 * x0 - st[L.head + k * a.C + c], b, fa);
+            for (int k = 0; k <= 15; ++k) emit(a, L, st, c, k, iir_step(zf, st[L.head + k * a.C + c], b, fa));
+        } else {
+            emit(a, L, st, c, i, iir_step(zf, bold, b, fa));
+        }
+        if (i == n - 1) {
+            // odd extension at the end: 2 x[n-1] - x[n-2..n-16]; backward pass starts there
+            const double xl = st[L.x16 + 15 * a.C + c];
+            double yext[kPad];
+#pragma unroll
+            for (int k = 0; k < kPad; ++k) yext[k] = iir_step(zf, 2.0 * xl - st[L.x16 + (14 - k) * a.C + c], b, fa);
+            double zb[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) zb[k] = a.cfg.zi[k] * yext[kPad - 1];
+#pragma unroll
+            for (int k = kPad - 1; k >= 0; --k) iir_step(zb, yext[k], b, fa);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) st[L.zend + k * a.C + c] = zb[k];
+        }
+    }
+    st[L.bal + c] = s;
+    st[L.bal + a.C + c] = f;
+    st[L.bal + 2 * a.C + c] = v;
+    st[L.bal + 3 * a.C + c] = q;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st[L.zf + k * a.C + c] = zf[k];
+}
+
+__global__ void bold_init_kernel(int64_t C, double* st) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    st[c] = 0.0;          // s
+    st[C + c] = 1.0;      // f
+    st[2 * C + c] = 1.0;  // v
+    st[3 * C + c] = 1.0;  // q
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st[4 * C + k * C + c] = 0.0;
+}
+
+// ---- block combination in the filter's modal basis, double-double ----
+// In the DF2T state basis the companion matrix A is violently non-normal
+// (|A^1000| ~ 3e7 for this band-pass), so propagating block-boundary states
+// as z <- A^L z + u amplifies rounding at every block.  In the eigenbasis
+// A = V diag(lam) V^-1 the propagation is a contraction (|lam|^1000 <= 0.1);
+// V (cond ~2e7) is only applied through double-double arithmetic, so the
+// combination adds nothing above filtfilt's own fp64 rounding noise.
+#pragma clang fp contract(off)
+struct dd { double hi, lo; };
+struct cdd { dd re, im; };
+__host__ __device__ inline dd two_sum(double a, double b) {
+    const double s = a + b, bb = s - a;
+    return {s, (a - (s - bb)) + (b - bb)};
+}
+__host__ __device__ inline dd quick_two_sum(double a, double b) {
+    const double s = a + b;
+    return {s, b - (s - a)};
+}
+__host__ __device__ inline dd dd_add(dd x, dd y) {
+    dd s = two_sum(x.hi, y.hi), t = two_sum(x.lo, y.lo);
+    s.lo += t.hi;
+    s = quick_two_sum(s.hi, s.lo);
+    s.lo += t.lo;
+    return quick_two_sum(s.hi, s.lo);
+}
+__host__ __device__ inline dd dd_neg(dd x) { return {-x.hi, -x.lo}; }
+__host__ __device__ inline dd dd_mul(dd x, dd y) {
+    const double p = x.hi * y.hi;
+    double e = fma(x.hi, y.hi, -p);
+    e += x.hi * y.lo + x.lo * y.hi;
+    return quick_two_sum(p, e);
+}
+__host__ __device__ inline dd dd_mul_d(dd x, double d) {
+    const double p = x.hi * d;
+    double e = fma(x.hi, d, -p);
+    e += x.lo * d;
+    return quick_two_sum(p, e);
+}
+__host__ __device__ inline cdd cdd_mul(cdd a, cdd b) {
+    return {dd_add(dd_mul(a.re, b.re), dd_neg(dd_mul(a.im, b.im))), dd_add(dd_mul(a.re, b.im), dd_mul(a.im, b.re))};
+}
+__host__ __device__ inline cdd cdd_add(cdd a, cdd b) { return {dd_add(a.re, b.re), dd_add(a.im, b.im)}; }
+__host__ __device__ inline cdd cdd_mul_d(cdd a, double d) { return {dd_mul_d(a.re, d), dd_mul_d(a.im, d)}; }
+#pragma clang fp contract(on)
+
+struct FinishArgs {
+    int64_t C, M, dec;
+    cdd Vi[16];             // V^-1 (row-major)
+    cdd lamL[4], lamL1[4];  // lam^dec, lam^(dec-1)
+    cdd lamT[4], lamT1[4];  // the same for the last (possibly short) block
+};
+
+__global__ void bold_finish_kernel(const FinishArgs f, const double* __restrict__ st, double* __restrict__ out) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= f.C) return;
+    const BoldLayout L(f.C, f.M, f.dec);
+    // w = V^-1 z_end
+    double z[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[k] = st[L.zend + k * f.C + c];
+    cdd w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        cdd acc = {{0, 0}, {0, 0}};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc = cdd_add(acc, cdd_mul_d(f.Vi[i * 4 + k], z[k]));
+        w[i] = acc;
+    }
+    for (int64_t m = f.M - 1; m >= 0; --m) {
+        const bool last = m == f.M - 1;
+        // output at the block start: y_zs + c V lam^(L-1) w, and c V = (1, 1, 1, 1)
+        dd y = {st[L.yzs + m * f.C + c], 0.0};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y = dd_add(y, cdd_mul(last ? f.lamT1[i] : f.lamL1[i], w[i]).re);
+        out[m * f.C + c] = y.hi + y.lo;
+        // w <- lam^L w + V^-1 u_m
+        double u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = st[L.u + (m * 4 + k) * f.C + c];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            cdd acc = cdd_mul(last ? f.lamT[i] : f.lamL[i], w[i]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc = cdd_add(acc, cdd_mul_d(f.Vi[i * 4 + k], u[k]));
+            w[i] = acc;
+        }
+    }
+}
+
+// ---------------- Hilbert phases (utils.kuramoto's hilbert, axis 0) ----------------
+// imag(hilbert(x))[t] = sum_tau x[tau] q[(t - tau) mod M],  q[d] = (2/M) sum_{k=1}^{K} sin(2 pi k d / M)
+// (K = M/2 - 1 for even M, (M-1)/2 for odd): the analytic signal's real part is
+// x itself.  Output: unit phasor (cos, sin) of angle(x + i H) per [t][c].
+constexpr int kHilNodes = 8;    // columns per workgroup
+constexpr int kHilT = 32;       // time slices per column
+__global__ void __launch_bounds__(256) hilbert_phase_kernel(int64_t C, int M, const double* __restrict__ x,
+                                                            const double* __restrict__ qk,
+                                                            double* __restrict__ ph) {
+    extern __shared__ double sq[];  // q[0..M)
+    for (int i = threadIdx.x; i < M; i += blockDim.x) sq[i] = qk[i];
+    __syncthreads();
+    const int lc = threadIdx.x % kHilNodes, ts = threadIdx.x / kHilNodes;
+    const int64_t c = (int64_t)blockIdx.x * kHilNodes + lc;
+    if (c >= C) return;
+    const int per = (M + kHilT - 1) / kHilT;
+    const int tb = ts * per, te = min(M, tb + per);
+    double acc[16];
+    for (int t0 = tb; t0 < te; t0 += 16) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[k] = 0.0;
+        for (int tau = 0; tau < M; ++tau) {
+            const double xv = x[(int64_t)tau * C + c];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                int d = t0 + k - tau;
+                d += d < 0 ? M : 0;
+                acc[k] += xv * sq[d < M ? d : 0];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int t = t0 + k;
+            if (t < te) {
+                const double re = x[(int64_t)t * C + c];
+                const double r = sqrt(re * re + acc[k] * acc[k]);
+                ph[((int64_t)t * C + c) * 2] = r > 0 ? re / r : 1.0;  // numpy: angle(0) = 0
+                ph[((int64_t)t * C + c) * 2 + 1] = r > 0 ? acc[k] / r : 0.0;
+            }
+        }
+    }
+}
+
+// q[d] = (2/M) sum_{k=1}^{K} sin(2 pi k d / M), exact (k d mod M) reduction
+__global__ void hilbert_kernel_q(int M, double* q) {
+    const int d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= M) return;
+    const int K = (M % 2 == 0) ? M / 2 - 1 : (M - 1) / 2;
+    double s = 0;
+    for (int k = 1; k <= K; ++k) s += sinpi(2.0 * (double)((int64_t)k * d % M) / M);
+    q[d] = 2.0 * s / M;
+}
+
+// ---------------- per-simulation FC, goodness of fit, mean, Kuramoto ----------------
+constexpr int kFcThreads = 256;
+
+__device__ double block_sum(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    double s = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+    __syncthreads();
+    return s;
+}
+
+struct FcArgs {
+    int B, N, M, K;
+    const double* bold;   // [M][B][N] band-passed, decimated BOLD (NULL: take fc_in)
+    const double* fc_in;  // [B][N][N] precomputed FC (used when bold == NULL)
+    const double* emp;    // [K][N][N]
+    const double* ph;     // [M][B][N][2] Hilbert phasors (may be NULL)
+    double* fc;           // [B][N][N] (may be NULL)
+    double* metrics;      // [B][K][4]: corr, euc, ssim, new_metric
+    double* extra;        // [B][3]: mean(FC), sync, meta
+};
+
+// LDS: fc[N*N] | emp[N*N] (also the time-chunk staging area before emp is loaded) | red[8]
+__global__ void __launch_bounds__(kFcThreads) fc_metrics_kernel(const FcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int N = a.N, M = a.M, NN = N * N;
+    double* fc = lds;
+    double* emp = lds + NN;
+    double* red = lds + 2 * NN;
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int64_t C = (int64_t)a.B * N;
+    const double* xb = a.bold ? a.bold + (int64_t)b * N : nullptr;
+
+    if (!a.bold) {
+        for (int i = tid; i < NN; i += blockDim.x) fc[i] = a.fc_in[(int64_t)b * NN + i];
+        __syncthreads();
+    } else {
+    // ---- np.cov: node means, centred cross products, 1/(M-1) ----
+    double* mean = red + 8;  // [N] after red
+    for (int n = tid; n < N; n += blockDim.x) {
+        double s = 0;
+        for (int t = 0; t < M; ++t) s += xb[(int64_t)t * C + n];
+        mean[n] = s / M;
+    }
+    __syncthreads();
+    // pairs (i <= j) distributed over threads; time staged through LDS (emp area)
+    const int npairs = N * (N + 1) / 2;
+    constexpr int kMaxPairs = (96 * 97 / 2 + kFcThreads - 1) / kFcThreads;
+    double acc[kMaxPairs];
+#pragma unroll
+    for (int k = 0; k < kMaxPairs; ++k) acc[k] = 0.0;
+    const int TCH = NN / N;  // time samples per staging chunk (N*N doubles of room)
+    for (int t0 = 0; t0 < M; t0 += TCH) {
+        const int tn = min(TCH, M - t0);
+        for (int i = tid; i < tn * N; i += blockDim.x) {
+            const int tt = i / N, n = i % N;
+            emp[i] = xb[(int64_t)(t0 + tt) * C + n] - mean[n];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kMaxPairs; ++k) {
+            const int p = tid + k * kFcThreads;
+            if (p < npairs) {
+                // p -> (i, j), i <= j, row-major over the upper triangle
+                int i = (int)((2 * N + 1 - sqrt((double)(2 * N + 1) * (2 * N + 1) - 8.0 * p)) / 2);
+                while (i > 0 && i * (2 * N - i + 1) / 2 > p) --i;
+                while ((i + 1) * (2 * N - i) / 2 <= p) ++i;
+                const int j = i + (p - i * (2 * N - i + 1) / 2);
+                double s = acc[k];
+                for (int tt = 0; tt < tn; ++tt) s += emp[tt * N + i] * emp[tt * N + j];
+                acc[k] = s;
+            }
+        }
+        __syncthreads();
+    }
+    const double fact = 1.0 / (M - 1);
+#pragma unroll
+    for (int k = 0; k < kMaxPairs; ++k) {
+        const int p = tid + k * kFcThreads;
+        if (p < npairs) {
+            int i = (int)((2 * N + 1 - sqrt((double)(2 * N + 1) * (2 * N + 1) - 8.0 * p)) / 2);
+            while (i > 0 && i * (2 * N - i + 1) / 2 > p) --i;
+            while ((i + 1) * (2 * N - i) / 2 <= p) ++i;
+            const int j = i + (p - i * (2 * N - i + 1) / 2);
+            const double cv = acc[k] * fact;
+            fc[i * N + j] = cv;
+            fc[j * N + i] = cv;
+        }
+    }
+    __syncthreads();
+    // ---- corrcoef: c /= sd[:,None]; c /= sd[None,:]; clip to [-1, 1] ----
+    double* sd = emp;  // reuse
+    for (int n = tid; n < N; n += blockDim.x) sd[n] = sqrt(fc[n * N + n]);
+    __syncthreads();
+    for (int i = tid; i < NN; i += blockDim.x) {
+        const int r = i / N, q = i % N;
+        double v = fc[i] / sd[r];
+        v = v / sd[q];
+        fc[i] = fmin(1.0, fmax(-1.0, v));
+    }
+    __syncthreads();
+    }
+    if (a.fc)
+        for (int i = tid; i < NN; i += blockDim.x) a.fc[(int64_t)b * NN + i] = fc[i];
+    // ---- mean(sFC) over all N^2 entries ----
+    double s = 0;
+    for (int i = tid; i < NN; i += blockDim.x) s += fc[i];
+    const double fcmean = block_sum(s, red) / NN;
+
+    // ---- goodness of fit against each empirical FC ----
+    const int nflat = N * (N - 1) / 2;
+    const int P = N - 6;  // SSIM interior (crop (7-1)/2 on each side)
+    for (int k = 0; k < a.K; ++k) {
+        for (int i = tid; i < NN; i += blockDim.x) emp[i] = a.emp[(int64_t)k * NN + i];
+        __syncthreads();
+        // flat upper triangles: means, then centred sums (np.corrcoef of two vectors)
+        double sx = 0, sy = 0;
+        for (int p = tid; p < NN; p += blockDim.x) {
+            const int r = p / N, q = p % N;
+            if (q > r) { sx += fc[p]; sy += emp[p]; }
+        }
+        const double mx = block_sum(sx, red) / nflat;
+        const double my = block_sum(sy, red) / nflat;
+        double sxx = 0, syy = 0, sxy = 0, see = 0;
+        for (int p = tid; p < NN; p += blockDim.x) {
+            const int r = p / N, q = p % N;
+            if (q > r) {
+                const double dx = fc[p] - mx, dy = emp[p] - my, de = emp[p] - fc[p];
+                sxx += dx * dx;
+                syy += dy * dy;
+                sxy += dx * dy;
+                see += de * de;
+            }
+        }
+        sxx = block_sum(sxx, red);
+        syy = block_sum(syy, red);
+        sxy = block_sum(sxy, red);
+        see = block_sum(see, red);
+        const double f1 = 1.0 / (nflat - 1);
+        double corr = (sxy * f1) / sqrt(sxx * f1) / sqrt(syy * f1);
+        corr = fmin(1.0, fmax(-1.0, corr));
+        const double euc = sqrt(see);
+        const double newm = 1.0 - corr + (mx - my) * (mx - my);
+        // SSIM (skimage 0.18 defaults): 7x7 uniform filter of x, y, xx, yy, xy
+        // (row sums /7 then column sums /7), sample covariance 49/48, mean of the
+        // interior P x P map.  Thread = (output column, row band).
+        double ssum = 0;
+        const int nbands = (int)blockDim.x / P;
+        const int jcol = tid % P, band = tid / P;
+        if (band < nbands) {
+            const int j = jcol + 3;
+            const int r0 = 3 + (P * band) / nbands, r1 = 3 + (P * (band + 1)) / nbands;
+            const double C1 = 0.01 * 0.01, C2 = 0.03 * 0.03, cov_norm = 49.0 / 48.0;
+            for (int i = r0; i < r1; ++i) {
+                double vx = 0, vy = 0, vxx = 0, vyy = 0, vxy = 0;
+                for (int di = -3; di <= 3; ++di) {
+                    const int r = i + di;
+                    double hx = 0, hy = 0, hxx = 0, hyy = 0, hxy = 0;
+                    for (int dj = -3; dj <= 3; ++dj) {
+                        const double xv = fc[r * N + j + dj], yv = emp[r * N + j + dj];
+                        hx += xv;
+                        hy += yv;
+                        hxx += xv * xv;
+                        hyy += yv * yv;
+                        hxy += xv * yv;
+                    }
+                    vx += hx / 7.0;
+                    vy += hy / 7.0;
+                    vxx += hxx / 7.0;
+                    vyy += hyy / 7.0;
+                    vxy += hxy / 7.0;
+                }
+                const double ux = vx / 7.0, uy = vy / 7.0, uxx = vxx / 7.0, uyy = vyy / 7.0, uxy = vxy / 7.0;
+                const double sx2 = cov_norm * (uxx - ux * ux), sy2 = cov_norm * (uyy - uy * uy),
+                             sxy2 = cov_norm * (uxy - ux * uy);
+                const double A1 = 2 * ux * uy + C1, A2 = 2 * sxy2 + C2;
+                const double B1 = ux * ux + uy * uy + C1, B2 = sx2 + sy2 + C2;
+                ssum += (A1 * A2) / (B1 * B2);
+            }
+        }
+        const double ssim = block_sum(ssum, red) / ((double)P * P);
+        if (tid == 0) {
+            double* o = a.metrics + ((int64_t)b * a.K + k) * 4;
+            o[0] = corr;
+            o[1] = euc;
+            o[2] = ssim;
+            o[3] = newm;
+        }
+        __syncthreads();
+    }
+    // ---- Kuramoto order parameter R(t) = |mean_n exp(i theta_n(t))|: mean and std ----
+    double sync = 0, meta = 0;
+    if (a.ph) {
+        double r1 = 0, r2 = 0;
+        for (int t = tid; t < M; t += blockDim.x) {
+            double cr = 0, ci = 0;
+            const double* p = a.ph + ((int64_t)t * C + (int64_t)b * N) * 2;
+            for (int n = 0; n < N; ++n) {
+                cr += p[2 * n];
+                ci += p[2 * n + 1];
+            }
+            cr /= N;
+            ci /= N;
+            const double R = sqrt(cr * cr + ci * ci);
+            r1 += R;
+            emp[t] = R;  // emp is free now
+        }
+        sync = block_sum(r1, red) / M;
+        for (int t = tid; t < M; t += blockDim.x) r2 += (emp[t] - sync) * (emp[t] - sync);
+        meta = sqrt(block_sum(r2, red) / M);
+    }
+    if (tid == 0) {
+        a.extra[b * 3 + 0] = fcmean;
+        a.extra[b * 3 + 1] = sync;
+        a.extra[b * 3 + 2] = meta;
+    }
+}
+
+// ---- host: poles, eigenvectors and their inverse in long double ----
+typedef std::complex<long double> cld;
+
+cdd to_cdd(cld x) {
+    const long double r = x.real(), i = x.imag();
+    const double rh = (double)r, ih = (double)i;
+    return {{rh, (double)(r - rh)}, {ih, (double)(i - ih)}};
+}
+
+// roots of z^4 + a1 z^3 + a2 z^2 + a3 z + a4 (Durand-Kerner, then Newton polish)
+void poles(const double* a, cld lam[4]) {
+    auto P = [&](cld z) { return (((z + (long double)a[1]) * z + (long double)a[2]) * z + (long double)a[3]) * z + (long double)a[4]; };
+    auto dP = [&](cld z) { return ((4.0L * z + 3.0L * (long double)a[1]) * z + 2.0L * (long double)a[2]) * z + (long double)a[3]; };
+    const cld seed(0.4L, 0.9L);
+    cld r[4] = {1.0L, seed, seed * seed, seed * seed * seed};
+    for (int it = 0; it < 2000; ++it) {
+        long double delta = 0;
+        for (int i = 0; i < 4; ++i) {
+            cld den = 1.0L;
+            for (int j = 0; j < 4; ++j)
+                if (j != i) den *= (r[i] - r[j]);
+            const cld d = P(r[i]) / den;
+            r[i] -= d;
+            delta = std::max(delta, std::abs(d));
+        }
+        if (delta < 1e-30L) break;
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int it = 0; it < 5; ++it) r[i] -= P(r[i]) / dP(r[i]);
+    for (int i = 0; i < 4; ++i) lam[i] = r[i];
+}
+
+// V[:, i] = (1, lam+a1, lam^2+a1 lam+a2, lam^3+a1 lam^2+a2 lam+a3) is the
+// eigenvector of the DF2T companion (A[k][0] = -a[k+1], A[k][k+1] = 1); invert it
+bool modal_inverse(const double* a, const cld lam[4], cld Vi[16]) {
+    cld M[4][8];
+    for (int i = 0; i < 4; ++i) {
+        const cld l = lam[i];
+        const cld v1 = l + (long double)a[1], v2 = l * v1 + (long double)a[2], v3 = l * v2 + (long double)a[3];
+        const cld col[4] = {1.0L, v1, v2, v3};
+        for (int r = 0; r < 4; ++r) M[r][i] = col[r];
+    }
+    for (int r = 0; r < 4; ++r)
+        for (int k = 0; k < 4; ++k) M[r][4 + k] = (r == k) ? 1.0L : 0.0L;
+    for (int col = 0; col < 4; ++col) {
+        int piv = col;
+        for (int r = col + 1; r < 4; ++r)
+            if (std::abs(M[r][col]) > std::abs(M[piv][col])) piv = r;
+        if (std::abs(M[piv][col]) == 0) return false;
+        for (int k = 0; k < 8; ++k) std::swap(M[col][k], M[piv][k]);
+        const cld d = M[col][col];
+        for (int k = 0; k < 8; ++k) M[col][k] /= d;
+        for (int r = 0; r < 4; ++r)
+            if (r != col) {
+                const cld fct = M[r][col];
+                for (int k = 0; k < 8; ++k) M[r][k] -= fct * M[col][k];
+            }
+    }
+    for (int r = 0; r < 4; ++r)
+        for (int k = 0; k < 4; ++k) Vi[r * 4 + k] = M[r][4 + k];
+    return true;
+}
+
+cld cpow_int(cld x, int64_t p) {
+    cld r = 1.0L;
+    while (p > 0) {
+        if (p & 1) r *= x;
+        x *= x;
+        p >>= 1;
+    }
+    return r;
+}
+
+int check_cfg(const wc_bold_cfg* cfg, int64_t C) {
+    if (!cfg || C <= 0 || cfg->dec <= 0 || cfg->neq < 0 || cfg->n_total - cfg->neq < 16)
+        return wc_set_err(WC_EINVAL, "wc_bold: invalid configuration (need n_total - neq >= 16)");
+    if (cfg->a[0] != 1.0) return wc_set_err(WC_EINVAL, "wc_bold: a[0] must be 1");
+    return WC_OK;
+}
+
+BoldArgs make_bold_args(const wc_bold_cfg* cfg, int64_t C) {
+    BoldArgs a;
+    a.cfg = *cfg;
+    a.C = C;
+    a.n = cfg->n_total - cfg->neq;
+    a.M = (a.n + cfg->dec - 1) / cfg->dec;
+    // Balloon-Windkessel constants (assumed BD.Sim; DESIGN.md "BOLD model")
+    a.itaus = 1.0 / 0.65;
+    a.itauf = 1.0 / 0.41;
+    a.itauo = 1.0 / 0.98;
+    a.ialpha = 1.0 / 0.32;
+    a.Eo = 0.4;
+    a.vo = 0.04;
+    a.k1 = 7.0 * a.Eo;
+    a.k2 = 2.0;
+    a.k3 = 2.0 * a.Eo - 0.2;
+    a.log1mEo = log(1.0 - a.Eo);
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t wc_bold_blocks(const wc_bold_cfg* cfg) {
+    if (!cfg || cfg->dec <= 0 || cfg->n_total <= cfg->neq) return 0;
+    return (cfg->n_total - cfg->neq + cfg->dec - 1) / cfg->dec;
+}
+
+size_t wc_bold_state_doubles(const wc_bold_cfg* cfg, int64_t C) {
+    if (!cfg || cfg->dec <= 0 || C <= 0) return 0;
+    return (size_t)BoldLayout(C, wc_bold_blocks(cfg), cfg->dec).total;
+}
+
+int wc_bold_init(const wc_bold_cfg* cfg, int64_t C, double* state, void* stream) {
+    wc_clear_err();
+    int rc = check_cfg(cfg, C);
+    if (rc) return rc;
+    if (!state) return wc_set_err(WC_EINVAL, "wc_bold_init: NULL state");
+    hipLaunchKernelGGL(bold_init_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), C, state);
+    return wc_hip_check("wc_bold_init");
+}
+
+int wc_bold_chunk(const wc_bold_cfg* cfg, int64_t C, const void* E, int e_f64, int64_t e_ld, int64_t t0,
+                  int64_t Tc, double* state, void* stream) {
+    wc_clear_err();
+    int rc = check_cfg(cfg, C);
+    if (rc) return rc;
+    if (!E || !state || t0 < 0 || Tc < 0 || t0 + Tc > cfg->n_total || e_ld < 0 || (e_ld > 0 && e_ld < Tc))
+        return wc_set_err(WC_EINVAL, "wc_bold_chunk: bad E/state/t0/Tc");
+    if (Tc == 0) return WC_OK;
+    const BoldArgs a = make_bold_args(cfg, C);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)((C + 255) / 256));
+    if (e_f64)
+        hipLaunchKernelGGL(bold_chunk_kernel<double>, grid, dim3(256), 0, st, a, static_cast<const double*>(E), e_ld,
+                           t0, Tc, state);
+    else
+        hipLaunchKernelGGL(bold_chunk_kernel<float>, grid, dim3(256), 0, st, a, static_cast<const float*>(E), e_ld, t0,
+                           Tc, state);
+    return wc_hip_check("wc_bold_chunk");
+}
+
+int wc_bold_finish(const wc_bold_cfg* cfg, int64_t C, const double* state, double* out, void* stream) {
+    wc_clear_err();
+    int rc = check_cfg(cfg, C);
+    if (rc) return rc;
+    if (!state || !out) return wc_set_err(WC_EINVAL, "wc_bold_finish: NULL argument");
+    FinishArgs f;
+    f.C = C;
+    f.dec = cfg->dec;
+    const int64_t n = cfg->n_total - cfg->neq;
+    f.M = (n + cfg->dec - 1) / cfg->dec;
+    const int64_t Llast = n - (f.M - 1) * cfg->dec;
+    cld lam[4], Vi[16];
+    poles(cfg->a, lam);
+    if (!modal_inverse(cfg->a, lam, Vi)) return wc_set_err(WC_EINVAL, "wc_bold_finish: degenerate filter");
+    for (int i = 0; i < 16; ++i) f.Vi[i] = to_cdd(Vi[i]);
+    if (getenv("WCSDE_DEBUG")) {
+        fprintf(stderr, "wc_bold_finish: a = %.17g %.17g %.17g %.17g %.17g dec=%lld M=%lld C=%lld\n", cfg->a[0],
+                cfg->a[1], cfg->a[2], cfg->a[3], cfg->a[4], (long long)cfg->dec, (long long)f.M, (long long)C);
+        for (int i = 0; i < 4; ++i)
+            fprintf(stderr, "  lam[%d] = %.20Lg %.20Lg   Vi[%d][0] = %Lg %Lg\n", i, lam[i].real(), lam[i].imag(), i,
+                    Vi[i * 4].real(), Vi[i * 4].imag());
+    }
+    for (int i = 0; i < 4; ++i) {
+        f.lamL[i] = to_cdd(cpow_int(lam[i], cfg->dec));
+        f.lamL1[i] = to_cdd(cpow_int(lam[i], cfg->dec - 1));
+        f.lamT[i] = to_cdd(cpow_int(lam[i], Llast));
+        f.lamT1[i] = to_cdd(cpow_int(lam[i], Llast - 1));
+    }
+    hipLaunchKernelGGL(bold_finish_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), f, state, out);
+    return wc_hip_check("wc_bold_finish");
+}
+
+int wc_hilbert_phase(int64_t C, int M, const double* x, double* phasor, void* workspace, size_t ws_bytes,
+                     void* stream) {
+    wc_clear_err();
+    if (C <= 0 || M <= 1 || !x || !phasor) return wc_set_err(WC_EINVAL, "wc_hilbert_phase: bad arguments");
+    if (!workspace || ws_bytes < (size_t)M * sizeof(double))
+        return wc_set_err(WC_EWORKSPACE, "wc_hilbert_phase: workspace < M doubles");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(hilbert_kernel_q, dim3((M + 255) / 256), dim3(256), 0, st, M, static_cast<double*>(workspace));
+    const unsigned blocks = (unsigned)((C + kHilNodes - 1) / kHilNodes);
+    hipLaunchKernelGGL(hilbert_phase_kernel, dim3(blocks), dim3(kHilNodes * kHilT), M * sizeof(double), st, C, M, x,
+                       static_cast<const double*>(workspace), phasor);
+    return wc_hip_check("wc_hilbert_phase");
+}
+
+int wc_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, const double* empfc, int K,
+                  const double* phasor, double* fc_out, double* metrics, double* extra, void* stream) {
+    wc_clear_err();
+    if (B <= 0 || N < 7 || N > 96 || M < 2 || K < 0 || (!bold && !fc_in) || !extra ||
+        (K > 0 && (!empfc || !metrics)))
+        return wc_set_err(WC_EINVAL, "wc_fc_metrics: bad arguments (7 <= N <= 96)");
+    FcArgs a{B, N, M, K, bold, fc_in, empfc, phasor, fc_out, metrics, extra};
+    const size_t lds = (size_t)(2 * N * N + 8 + N) * sizeof(double);
+    hipError_t e = hipFuncSetAttribute((const void*)fc_metrics_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
+    hipLaunchKernelGGL(fc_metrics_kernel, dim3(B), dim3(kFcThreads), lds, static_cast<hipStream_t>(stream), a);
+    return wc_hip_check("wc_fc_metrics");
+}
+
+}  // extern "C"

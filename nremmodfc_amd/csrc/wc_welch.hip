@@ -1,0 +1,304 @@
+// wc_welch.hip -- Welch peak frequency of E_t for a batch of simulations (gfx950).
+//
+// Replaces whole_sweep_both.py:90-95:
+//   freqs, fftPow = signal.welch(E_t.T, fs=1/wc.dt, nperseg=4000)
+//   meanpow = fftPow.mean(axis=0); peakfreq = freqs[first argmax(meanpow)]
+// scipy.signal.welch defaults: periodic Hann window, noverlap = nperseg/2,
+// constant detrend per segment, density scaling, one-sided (bins 1..nperseg/2-1
+// doubled), mean over segments.
+//
+// One workgroup per simulation and segment set: for each node, the 4000-sample
+// segment is staged in LDS (node-major E: contiguous 4000-sample runs),
+// mean-removed and windowed, packed as 2000 complex points z[n] = x[2n] +
+// i x[2n+1], transformed by a Stockham FFT (radix 5, 5, 5, 4, 4) and unpacked
+// to the 2001 real-FFT bins; |X_k|^2 is summed over nodes in registers and
+// added to the simulation's fp64 accumulator row (single writer: deterministic).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include "wc_common.h"
+
+namespace {
+
+
+constexpr int kSeg = 4000;     // nperseg (whole_sweep_both.py:90)
+constexpr int kFFT = kSeg / 2; // packed complex length
+constexpr int kBins = kFFT + 1;
+constexpr int kThreads = 256;
+constexpr int kBinsPerThread = (kBins + kThreads - 1) / kThreads;  // 8
+
+template <typename R> struct cx { R re, im; };
+template <typename R> __device__ __forceinline__ cx<R> cmul(cx<R> a, cx<R> b) {
+    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+template <typename R> __device__ __forceinline__ cx<R> cadd(cx<R> a, cx<R> b) { return {a.re + b.re, a.im + b.im}; }
+template <typename R> __device__ __forceinline__ cx<R> csub(cx<R> a, cx<R> b) { return {a.re - b.re, a.im - b.im}; }
+
+// concurrent FFTs per workgroup: 2 x (ping + pong) x 2000 complex fits 64 KB (fp32) / 128 KB (fp64)
+template <typename R> constexpr int kG = sizeof(R) == 4 ? 4 : 2;
+
+// twiddle table T[m] = exp(-2 pi i m / 4000), m in [0, 4000)
+__global__ void twiddle_kernel(double* tw) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= kSeg) return;
+    double s, c;
+    sincospi(2.0 * m / kSeg, &s, &c);
+    tw[2 * m] = c;
+    tw[2 * m + 1] = -s;
+}
+
+template <typename R>
+__device__ __forceinline__ cx<R> tw_at(const double* tw, int m) {  // exp(-2 pi i m / 4000), m mod 4000
+    m %= kSeg;
+    return {(R)tw[2 * m], (R)tw[2 * m + 1]};
+}
+
+// one Stockham stage of radix RAD over the 2000-point FFT, p = product of previous radices
+template <typename R, int RAD>
+__device__ __forceinline__ void stage(const cx<R>* __restrict__ x, cx<R>* __restrict__ y, int p, int i,
+                                      const double* tw) {
+    constexpr int S = kFFT / RAD;
+    const int k = i % p;
+    cx<R> u[RAD];
+#pragma unroll
+    for (int r = 0; r < RAD; ++r) u[r] = x[i + r * S];
+    // twiddle exp(-2 pi i r k / (p RAD)) = T[2 * r * k * (kFFT / (p RAD))]
+    const int step = 2 * (kFFT / (p * RAD));
+#pragma unroll
+    for (int r = 1; r < RAD; ++r) u[r] = cmul(u[r], tw_at<R>(tw, r * k * step));
+    cx<R> U[RAD];
+    if constexpr (RAD == 4) {
+        const cx<R> a = cadd(u[0], u[2]), b = csub(u[0], u[2]);
+        const cx<R> c = cadd(u[1], u[3]), d = csub(u[1], u[3]);
+        U[0] = cadd(a, c);
+        U[2] = csub(a, c);
+        U[1] = {b.re + d.im, b.im - d.re};  // b - i d
+        U[3] = {b.re - d.im, b.im + d.re};  // b + i d
+    } else {  // RAD == 5
+        const R c1 = (R)0.30901699437494742410, c2 = (R)-0.80901699437494742410;  // cos(2pi/5), cos(4pi/5)
+        const R s1 = (R)0.95105651629515357212, s2 = (R)0.58778525229247312917;   // sin(2pi/5), sin(4pi/5)
+        const cx<R> t1 = cadd(u[1], u[4]), t2 = cadd(u[2], u[3]);
+        const cx<R> t3 = csub(u[1], u[4]), t4 = csub(u[2], u[3]);
+        U[0] = {u[0].re + t1.re + t2.re, u[0].im + t1.im + t2.im};
+        const cx<R> a1 = {u[0].re + c1 * t1.re + c2 * t2.re, u[0].im + c1 * t1.im + c2 * t2.im};
+        const cx<R> a2 = {u[0].re + c2 * t1.re + c1 * t2.re, u[0].im + c2 * t1.im + c1 * t2.im};
+        // -i (s1 t3 + s2 t4) and -i (s2 t3 - s1 t4)
+        const cx<R> b1 = {s1 * t3.re + s2 * t4.re, s1 * t3.im + s2 * t4.im};
+        const cx<R> b2 = {s2 * t3.re - s1 * t4.re, s2 * t3.im - s1 * t4.im};
+        U[1] = {a1.re + b1.im, a1.im - b1.re};
+        U[4] = {a1.re - b1.im, a1.im + b1.re};
+        U[2] = {a2.re + b2.im, a2.im - b2.re};
+        U[3] = {a2.re - b2.im, a2.im + b2.re};
+    }
+    const int j = (i - k) * RAD + k;
+#pragma unroll
+    for (int s = 0; s < RAD; ++s) y[j + s * p] = U[s];
+}
+
+template <typename R, int RAD>
+__device__ __forceinline__ void run_stage(cx<R>* const* src, cx<R>* const* dst, int p, const double* tw) {
+    constexpr int nb = kFFT / RAD;
+    for (int idx = threadIdx.x; idx < kG<R> * nb; idx += kThreads) {
+        const int g = idx / nb, i = idx % nb;
+        stage<R, RAD>(src[g], dst[g], p, i, tw);
+    }
+    __syncthreads();
+}
+
+struct WelchArgs {
+    int B, N;
+    const void* E;     // node-major ring: element (c, t) at c*ld + ((t/slot) % nslots)*slot + t % slot
+    int64_t ld, slot, nslots;
+    int64_t seg0;      // first sample of the segment
+    const double* tw;  // twiddle table
+    double* acc;       // [B][kBins] running sum over nodes and segments of |X_k|^2
+};
+
+template <typename R>
+__global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cx<R>* base = reinterpret_cast<cx<R>*>(smem);  // [kG][2][kFFT]
+    R* red = reinterpret_cast<R*>(base + 2 * kG<R> * kFFT);  // [4 waves][kG]
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const R* E = static_cast<const R*>(a.E);
+    cx<R>* buf0[kG<R>];
+    cx<R>* buf1[kG<R>];
+#pragma unroll
+    for (int g = 0; g < kG<R>; ++g) {
+        buf0[g] = base + (2 * g) * kFFT;
+        buf1[g] = base + (2 * g + 1) * kFFT;
+    }
+    double acc[kBinsPerThread];
+#pragma unroll
+    for (int j = 0; j < kBinsPerThread; ++j) acc[j] = 0.0;
+
+    for (int n0 = 0; n0 < a.N; n0 += kG<R>) {
+        // ---- stage the raw segments (as reals) and their sums ----
+        R part[kG<R>];
+#pragma unroll
+        for (int g = 0; g < kG<R>; ++g) {
+            part[g] = 0;
+            const int n = n0 + g;
+            R* xr = reinterpret_cast<R*>(buf0[g]);
+            if (n < a.N) {
+                const R* col = E + ((int64_t)b * a.N + n) * a.ld;
+                // the segment is <= 5 contiguous runs of the ring (wave-uniform bookkeeping)
+                for (int t = 0; t < kSeg;) {
+                    const int64_t ts = a.seg0 + t;
+                    const int64_t q = ts / a.slot, r = ts % a.slot;
+                    const int len = (int)min((int64_t)(kSeg - t), a.slot - r);
+                    const R* src = col + (q % a.nslots) * a.slot + r;
+                    for (int i = tid; i < len; i += kThreads) {
+                        const R v = src[i];
+                        xr[t + i] = v;
+                        part[g] += v;
+                    }
+                    t += len;
+                }
+            } else {
+                for (int t = tid; t < kSeg; t += kThreads) xr[t] = 0;
+            }
+        }
+        // block reduction of the kG sums (wave shuffles, then 4 partials per g)
+#pragma unroll
+        for (int g = 0; g < kG<R>; ++g) {
+            R v = part[g];
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if ((tid & 63) == 0) red[(tid >> 6) * kG<R> + g] = v;
+        }
+        __syncthreads();
+        R mean[kG<R>];
+#pragma unroll
+        for (int g = 0; g < kG<R>; ++g)
+            mean[g] = (red[g] + red[kG<R> + g] + red[2 * kG<R> + g] + red[3 * kG<R> + g]) / (R)kSeg;
+        // ---- detrend, periodic Hann window, pack z[n] = x[2n] + i x[2n+1] (in place) ----
+#pragma unroll
+        for (int g = 0; g < kG<R>; ++g) {
+            cx<R>* z = buf0[g];
+            for (int m = tid; m < kFFT; m += kThreads) {
+                const cx<R> v = z[m];
+                const R w0 = (R)(0.5 - 0.5 * a.tw[2 * (2 * m)]);
+                const R w1 = (R)(0.5 - 0.5 * a.tw[2 * (2 * m + 1)]);
+                z[m] = {w0 * (v.re - mean[g]), w1 * (v.im - mean[g])};
+            }
+        }
+        __syncthreads();
+        // ---- Stockham 2000 = 5 * 5 * 5 * 4 * 4 ----
+        run_stage<R, 5>(buf0, buf1, 1, a.tw);
+        run_stage<R, 5>(buf1, buf0, 5, a.tw);
+        run_stage<R, 5>(buf0, buf1, 25, a.tw);
+        run_stage<R, 4>(buf1, buf0, 125, a.tw);
+        run_stage<R, 4>(buf0, buf1, 500, a.tw);
+        // ---- unpack X_k = (Z_k + conj Z_{-k})/2 - i/2 W^k (Z_k - conj Z_{-k}), |X_k|^2 ----
+#pragma unroll
+        for (int j = 0; j < kBinsPerThread; ++j) {
+            const int k = tid + j * kThreads;
+            if (k < kBins) {
+#pragma unroll
+                for (int g = 0; g < kG<R>; ++g) {
+                    if (n0 + g >= a.N) continue;
+                    const cx<R> Zk = buf1[g][k % kFFT];
+                    const cx<R> Zc = buf1[g][(kFFT - k) % kFFT];
+                    const double er = 0.5 * ((double)Zk.re + Zc.re), ei = 0.5 * ((double)Zk.im - Zc.im);
+                    const double dr = (double)Zk.re - Zc.re, di = (double)Zk.im + Zc.im;
+                    const double wr = a.tw[2 * k], wi = a.tw[2 * k + 1];
+                    // -i/2 * W * d
+                    const double pr = wr * dr - wi * di, pi = wr * di + wi * dr;
+                    const double xr = er + 0.5 * pi, xi = ei - 0.5 * pr;
+                    acc[j] += xr * xr + xi * xi;
+                }
+            }
+        }
+        __syncthreads();  // buffers reused by the next node group
+    }
+#pragma unroll
+    for (int j = 0; j < kBinsPerThread; ++j) {
+        const int k = tid + j * kThreads;
+        if (k < kBins) a.acc[(int64_t)b * kBins + k] += acc[j];
+    }
+}
+
+// mean PSD (density scaling, one-sided) and the first argmax -> peak frequency
+__global__ void welch_peak_kernel(int B, int N, int nseg, double fs, const double* __restrict__ acc,
+                                  double* __restrict__ peak, double* __restrict__ psd) {
+    __shared__ double bv[kThreads];
+    __shared__ int bi[kThreads];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    // scale = 1/(fs * sum(w^2)); sum of the periodic Hann squared = 3/8 * nperseg
+    const double scale = 1.0 / (fs * (3.0 / 8.0) * kSeg) / ((double)nseg * N);
+    double best = -1.0;
+    int besti = 0;
+    for (int k = tid; k < kBins; k += kThreads) {
+        double v = acc[(int64_t)b * kBins + k] * scale;
+        if (k > 0 && k < kBins - 1) v *= 2.0;
+        if (psd) psd[(int64_t)b * kBins + k] = v;
+        if (v > best) { best = v; besti = k; }
+    }
+    bv[tid] = best;
+    bi[tid] = besti;
+    __syncthreads();
+    for (int s = kThreads / 2; s > 0; s >>= 1) {
+        if (tid < s) {
+            if (bv[tid + s] > bv[tid] || (bv[tid + s] == bv[tid] && bi[tid + s] < bi[tid])) {
+                bv[tid] = bv[tid + s];
+                bi[tid] = bi[tid + s];
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) peak[b] = bi[0] * fs / kSeg;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t wc_welch_workspace_size(void) { return (size_t)kSeg * 2 * sizeof(double); }
+int wc_welch_bins(void) { return kBins; }
+
+int wc_welch_prepare(void* workspace, size_t ws_bytes, void* stream) {
+    wc_clear_err();
+    if (!workspace || ws_bytes < wc_welch_workspace_size()) return wc_set_err(WC_EWORKSPACE, "wc_welch_prepare");
+    hipLaunchKernelGGL(twiddle_kernel, dim3((kSeg + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<double*>(workspace));
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
+}
+
+int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int64_t slot, int64_t nslots,
+                        int64_t seg0, const void* workspace, double* acc, void* stream) {
+    wc_clear_err();
+    if (B <= 0 || N <= 0 || !E || !acc || !workspace || slot <= 0 || nslots <= 0 || seg0 < 0 || ld < slot * nslots ||
+        kSeg > slot * nslots)
+        return wc_set_err(WC_EINVAL, "wc_welch_accumulate: bad arguments");
+    WelchArgs a{B, N, E, ld, slot, nslots, seg0, static_cast<const double*>(workspace), acc};
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (e_f64) {
+        const size_t lds = (size_t)2 * kG<double> * kFFT * sizeof(cx<double>) + 4 * kG<double> * sizeof(double);
+        hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<double>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
+        hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
+    } else {
+        const size_t lds = (size_t)2 * kG<float> * kFFT * sizeof(cx<float>) + 4 * kG<float> * sizeof(float);
+        hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<float>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
+        hipLaunchKernelGGL(welch_kernel<float>, dim3(B), dim3(kThreads), lds, st, a);
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
+}
+
+int wc_welch_peak(int B, int N, int nseg, double fs, const double* acc, double* peak, double* psd, void* stream) {
+    wc_clear_err();
+    if (B <= 0 || N <= 0 || nseg <= 0 || !acc || !peak) return wc_set_err(WC_EINVAL, "wc_welch_peak: bad arguments");
+    hipLaunchKernelGGL(welch_peak_kernel, dim3(B), dim3(kThreads), 0, static_cast<hipStream_t>(stream), B, N, nseg,
+                       fs, acc, peak, psd);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
+}
+
+}  // extern "C"

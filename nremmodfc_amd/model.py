@@ -147,18 +147,24 @@ class Batch:
         return torch.float32 if self.precision == F32 else torch.float64
 
     def integrate(self, nsteps: int, tau_ip: float, rec_every: int = 0, recE=None, recI=None,
-                  recA=None, stream=None):
-        """Advance every simulation by nsteps (one wc_integrate call)."""
+                  recA=None, stream=None, rec_ld: int = 0):
+        """Advance every simulation by nsteps (one wc_integrate call).
+
+        rec_ld = 0: records land time-major [n_rec][B][N]; rec_ld > 0: node-major,
+        record k of column c = b*N + n at flat index c*rec_ld + k of the buffer
+        (the buffer may be a view starting at a ring slot).
+        """
         L = _lib.lib()
         if rec_every:
             n_rec = -(-nsteps // rec_every)
+            need = n_rec * self.B * self.N if rec_ld == 0 else (self.B * self.N - 1) * rec_ld + n_rec
             for r in (recE, recI, recA):
-                if r is not None and (r.dtype != self.rec_dtype or r.numel() < n_rec * self.B * self.N):
+                if r is not None and (r.dtype != self.rec_dtype or r.numel() < need):
                     raise ValueError("record buffer has the wrong dtype or is too small")
         rc = L.wc_integrate(ctypes.byref(self._pc), _PREC[self.precision], self.B, self.N,
                             _lib.ptr(self.sc), _lib.ptr(self.G), _lib.ptr(self.sigmaE),
                             _lib.ptr(self.keys), _lib.ptr(self.E), _lib.ptr(self.I), _lib.ptr(self.A),
-                            self.step, nsteps, float(tau_ip), rec_every, _lib.ptr(recE),
+                            self.step, nsteps, float(tau_ip), rec_every, rec_ld, _lib.ptr(recE),
                             _lib.ptr(recI), _lib.ptr(recA), _lib.ptr(self.ws), self.ws.numel(),
                             _lib.stream_handle(stream))
         _lib.check(rc, "wc_integrate")

@@ -1,0 +1,162 @@
+"""Device-side signal chain: BOLD + band-pass filtfilt + decimation, FC and
+goodness of fit, Kuramoto, Welch peak -- thin wrappers over libwcsde.so.
+
+References: simBOLD netwWilsonCowanPlastic.py:140-158; np.corrcoef
+whole_sweep_both.py:81; utils.get_all_metrics / kuramoto utils.py:34-50; Welch
+peak whole_sweep_both.py:90-95.  Every array stays on the device; columns are
+c = b*N + n.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .filters import bold_band, lfilter_zi
+
+NEQ = 2000          # wc:145
+WELCH_NPERSEG = 4000  # whole_sweep_both.py:90
+WELCH_HOP = WELCH_NPERSEG // 2
+
+
+def _ptr_at(t, offset_elems=0):
+    """Device pointer to element `offset_elems` of a contiguous tensor."""
+    if not t.is_cuda or not t.is_contiguous():
+        raise _lib.WCSDEError("libwcsde takes contiguous device tensors only")
+    return ctypes.c_void_p(t.data_ptr() + offset_elems * t.element_size())
+
+
+class BoldStream:
+    """simBOLD for C columns fed in consecutive sample chunks (any chunking).
+
+    n_total = number of E samples per column (len(wc.time)); output after
+    finish(): [M][C] fp64 = filtfilt(b, a, BOLD[neq:], axis=0)[::dec].
+    """
+
+    def __init__(self, C, n_total, neq=NEQ, dec=1000, bold_dt=0.04, device="cuda"):
+        b, a = bold_band(bold_dt)
+        zi = lfilter_zi(b, a)
+        self.cfg = _lib.WCBoldCfgC(bold_dt, neq, n_total, dec, (ctypes.c_double * 5)(*b),
+                                   (ctypes.c_double * 5)(*a), (ctypes.c_double * 4)(*zi))
+        L = _lib.lib()
+        self.C, self.n_total, self.device = int(C), int(n_total), torch.device(device)
+        if n_total - neq < 16:
+            raise ValueError("simBOLD needs at least neq + 16 samples (filtfilt padlen 15)")
+        self.M = int(L.wc_bold_blocks(ctypes.byref(self.cfg)))
+        nd = L.wc_bold_state_doubles(ctypes.byref(self.cfg), self.C)
+        self.state = torch.empty(nd, dtype=torch.float64, device=self.device)
+        _lib.check(L.wc_bold_init(ctypes.byref(self.cfg), self.C, _lib.ptr(self.state), _lib.stream_handle()),
+                   "wc_bold_init")
+        self.t = 0
+
+    def feed(self, E, Tc=None, e_ld=0, offset=0):
+        """Feed the next Tc samples.  E time-major [Tc][C] (e_ld=0), or a node-major
+        buffer with sample tt of column c at flat index offset + c*e_ld + tt."""
+        if Tc is None:
+            Tc = E.shape[0]
+        f64 = E.dtype == torch.float64
+        if not f64 and E.dtype != torch.float32:
+            raise TypeError("E must be float32 or float64")
+        rc = _lib.lib().wc_bold_chunk(ctypes.byref(self.cfg), self.C, _ptr_at(E, offset), int(f64), e_ld, self.t,
+                                      Tc, _lib.ptr(self.state), _lib.stream_handle())
+        _lib.check(rc, "wc_bold_chunk")
+        self.t += Tc
+
+    def finish(self):
+        if self.t != self.n_total:
+            raise RuntimeError(f"BoldStream fed {self.t} of {self.n_total} samples")
+        out = torch.empty((self.M, self.C), dtype=torch.float64, device=self.device)
+        _lib.check(_lib.lib().wc_bold_finish(ctypes.byref(self.cfg), self.C, _lib.ptr(self.state), _lib.ptr(out),
+                                             _lib.stream_handle()), "wc_bold_finish")
+        return out
+
+
+def hilbert_phase(x):
+    """Unit phasors of hilbert(x, axis=0) for x [M][C] fp64 -> [M][C][2]."""
+    M, C = x.shape
+    ph = torch.empty((M, C, 2), dtype=torch.float64, device=x.device)
+    ws = torch.empty(M, dtype=torch.float64, device=x.device)
+    _lib.check(_lib.lib().wc_hilbert_phase(C, M, _lib.ptr(x.contiguous()), _lib.ptr(ph), _lib.ptr(ws),
+                                           ws.numel() * 8, _lib.stream_handle()), "wc_hilbert_phase")
+    return ph
+
+
+def fc_metrics(bold=None, B=None, N=None, empfc=None, fc_in=None, kuramoto=True, want_fc=False):
+    """Per simulation: FC (np.corrcoef(BOLD.T)), get_all_metrics vs each empfc,
+    mean(FC), Kuramoto sync/meta.
+
+    bold [M][B*N] or [M][B][N] fp64, or fc_in [B][N][N] instead.  empfc: [K][N][N]
+    tensor/array or None.  Returns (fc [B][N][N] | None, metrics [B][K][4], extra [B][3]).
+    """
+    L = _lib.lib()
+    if bold is not None:
+        M = bold.shape[0]
+        bold = bold.reshape(M, B * N).contiguous()
+        dev = bold.device
+    else:
+        fc_in = fc_in.contiguous()
+        B, N = fc_in.shape[0], fc_in.shape[1]
+        M, dev = 2, fc_in.device
+        kuramoto = False
+    K = 0 if empfc is None else int(empfc.shape[0])
+    emp = None if empfc is None else torch.as_tensor(np.asarray(empfc, dtype=np.float64)).to(dev).contiguous()
+    metrics = torch.empty((B, max(K, 1), 4), dtype=torch.float64, device=dev)
+    extra = torch.empty((B, 3), dtype=torch.float64, device=dev)
+    fc = torch.empty((B, N, N), dtype=torch.float64, device=dev) if want_fc else None
+    ph = hilbert_phase(bold) if kuramoto else None
+    rc = L.wc_fc_metrics(B, N, M, _lib.ptr(bold) if bold is not None else None, _lib.ptr(fc_in), _lib.ptr(emp), K,
+                         _lib.ptr(ph), _lib.ptr(fc), _lib.ptr(metrics), _lib.ptr(extra), _lib.stream_handle())
+    _lib.check(rc, "wc_fc_metrics")
+    return fc, metrics[:, :K], extra
+
+
+class WelchAccumulator:
+    """Running node-summed |FFT|^2 of 4000-sample Hann segments (welch, nperseg=4000)."""
+
+    def __init__(self, B, N, device="cuda"):
+        L = _lib.lib()
+        self.B, self.N, self.device = B, N, torch.device(device)
+        self.bins = L.wc_welch_bins()
+        self.ws = torch.empty(L.wc_welch_workspace_size() // 8, dtype=torch.float64, device=self.device)
+        _lib.check(L.wc_welch_prepare(_lib.ptr(self.ws), self.ws.numel() * 8, _lib.stream_handle()),
+                   "wc_welch_prepare")
+        self.acc = torch.zeros((B, self.bins), dtype=torch.float64, device=self.device)
+        self.nseg = 0
+
+    def accumulate(self, E, ld, slot, nslots, seg0):
+        """Add segment [seg0, seg0+4000) of every column of the node-major ring E."""
+        f64 = E.dtype == torch.float64
+        rc = _lib.lib().wc_welch_accumulate(self.B, self.N, _ptr_at(E), int(f64), ld, slot, nslots, seg0,
+                                            _lib.ptr(self.ws), _lib.ptr(self.acc), _lib.stream_handle())
+        _lib.check(rc, "wc_welch_accumulate")
+        self.nseg += 1
+
+    def peak(self, fs=500.0, want_psd=False):
+        peak = torch.empty(self.B, dtype=torch.float64, device=self.device)
+        psd = torch.empty((self.B, self.bins), dtype=torch.float64, device=self.device) if want_psd else None
+        _lib.check(_lib.lib().wc_welch_peak(self.B, self.N, self.nseg, fs, _lib.ptr(self.acc), _lib.ptr(peak),
+                                            _lib.ptr(psd), _lib.stream_handle()), "wc_welch_peak")
+        return peak, psd
+
+
+def welch_peak(E_t, fs=500.0, want_psd=False):
+    """whole_sweep_both.py:90-95 for E [T][B][N] (time-major): peak frequency per
+    simulation (and the node-mean PSD)."""
+    T, B, N = E_t.shape
+    nodemajor = E_t.reshape(T, B * N).t().contiguous()  # [C][T]
+    wa = WelchAccumulator(B, N, E_t.device)
+    nseg = (T - WELCH_NPERSEG) // WELCH_HOP + 1
+    for s in range(nseg):
+        wa.accumulate(nodemajor, T, T, 1, s * WELCH_HOP)
+    return wa.peak(fs, want_psd)
+
+
+def sim_bold(E_t, bold_downsamp=1000, neq=NEQ, bold_dt=0.04):
+    """simBOLD (wc:140-158) of E [T][C] (time-major, any C) -> [M][C] fp64."""
+    T = E_t.shape[0]
+    C = int(np.prod(E_t.shape[1:]))
+    bs = BoldStream(C, T, neq, bold_downsamp, bold_dt, E_t.device)
+    bs.feed(E_t.reshape(T, C).contiguous())
+    return bs.finish()

@@ -7,7 +7,7 @@ this package.  It restates the reference algorithm on the CPU in fp64:
     (S wc:72-74, wilsonCowan wc:77-83, run wc:86-137) with the build's Philox
     noise stream, and the Balloon-Windkessel BOLD stage (assumed form of the
     missing BOLDModel.BD.Sim, called at wc:144);
-  * signal.py (numpy): simBOLD's band-pass/filtfilt/decimation (wc:140-158),
+  * sigchain.py (numpy): simBOLD's band-pass/filtfilt/decimation (wc:140-158),
     corrcoef FC, utils.get_all_metrics / kuramoto (utils.py:24-50), the Welch
     peak frequency of the drivers (whole_sweep_both.py:90-95).
 """

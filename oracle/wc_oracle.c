@@ -203,3 +203,25 @@ void orc_bold(const double* rE, int64_t T, int N, double dt, double* out)
         }
     }
 }
+
+/* Direct-form-II-transposed IIR (scipy.signal.lfilter semantics, a[0] == 1),
+ * fp64, over n samples of each of m independent columns of x ([n][m] row-major).
+ * zi [order][m] in/out (final state), y [n][m]. */
+void orc_lfilter(const double* b, const double* a, int order, const double* x, int64_t n, int m,
+                 double* zi, double* y)
+{
+    for (int c = 0; c < m; ++c) {
+        double z[16];
+        for (int k = 0; k < order; ++k) z[k] = zi[(size_t)k * m + c];
+        for (int64_t i = 0; i < n; ++i) {
+            const double xi = x[(size_t)i * m + c];
+            /* association order of scipy's lfilter.c (z + x*b - y*a): the narrow
+             * band-pass is ill-conditioned, so rounding order shows at ~1e-9 */
+            const double yi = z[0] + xi * b[0];
+            for (int k = 0; k < order - 1; ++k) z[k] = z[k + 1] + xi * b[k + 1] - yi * a[k + 1];
+            z[order - 1] = xi * b[order] - yi * a[order];
+            y[(size_t)i * m + c] = yi;
+        }
+        for (int k = 0; k < order; ++k) zi[(size_t)k * m + c] = z[k];
+    }
+}

@@ -41,10 +41,16 @@ def test_invalid_arguments_fail_loudly():
     from nremmodfc_amd import _lib
     L = _lib.lib()
     p = _lib.WCParamsC()
-    rc = L.wc_integrate(ctypes.byref(p), 0, 0, 90, *([None] * 7), 0, 1, 1.0, 0, None, None, None,
+    rc = L.wc_integrate(ctypes.byref(p), 0, 0, 90, *([None] * 7), 0, 1, 1.0, 0, 0, None, None, None,
                         None, 0, None)
     assert rc == -1
     assert b"invalid" in L.wc_last_error()
-    rc = L.wc_integrate(ctypes.byref(p), 0, 4, 200, *([ctypes.c_void_p(16)] * 7), 0, 1, 1.0, 0,
+    rc = L.wc_integrate(ctypes.byref(p), 0, 4, 200, *([ctypes.c_void_p(16)] * 7), 0, 1, 1.0, 0, 0,
                         None, None, None, ctypes.c_void_p(16), 1 << 20, None)
     assert rc == -2
+    # the signal-chain entry points validate before touching the device too
+    cfg = _lib.WCBoldCfgC()
+    cfg.dec, cfg.neq, cfg.n_total = 1000, 2000, 2010  # fewer than neq + 16 samples
+    assert L.wc_bold_init(ctypes.byref(cfg), 10, ctypes.c_void_p(16), None) == -1
+    assert L.wc_fc_metrics(1, 200, 298, None, None, None, 0, None, None, None, None, None) == -1
+    assert L.wc_welch_bins() == 2001

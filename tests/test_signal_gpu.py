@@ -1,0 +1,147 @@
+"""HIP signal chain (libwcsde.so) vs the CPU oracle and the golden vectors.
+
+Tolerances:
+  * simBOLD (BOLD ODE + filtfilt + decimation), fp64: |d| <= 1e-7 * max|BOLD|.
+    The band-pass's DF2T recursion is ill-conditioned (companion matrix with
+    |A^1000| ~ 3e7): SciPy's own filtfilt sits 4e-9 from an extended-precision
+    evaluation, two association orders of the same fp64 recursion differ by
+    ~6e-9, and a 1-ulp change of the BOLD input (exp(log v / alpha) vs pow)
+    moves the output by 2-6e-8;
+  * FC: 1e-12; get_all_metrics, kuramoto, mean(FC): rtol 1e-9;
+  * Welch PSD: rtol 1e-9 (fp64 input), 2e-4 (fp32 input); peak frequency exact.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import oracle.sigchain as osg
+from nremmodfc_amd import datasets
+from nremmodfc_amd import sigchain as wsg
+from tests.golden.make_golden import inputs
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _e_like(T, C, seed):
+    rng = np.random.default_rng(seed)
+    t = np.arange(T) / 500.0
+    return (0.2 + 0.1 * np.sin(2 * np.pi * 4.8 * t)[:, None] * rng.uniform(0.5, 1.5, C)
+            + 0.03 * rng.standard_normal((T, C))).astype(np.float64)
+
+
+@pytest.mark.parametrize("T,dec,C", [(20_000, 1000, 6), (12_345, 1000, 3), (5_000, 10, 4), (300_000, 1000, 2)])
+def test_sim_bold_matches_oracle(cuda, T, dec, C):
+    E = _e_like(T, C, T + dec)
+    want = osg.sim_bold(E, bold_downsamp=dec)
+    got = wsg.sim_bold(torch.from_numpy(E).cuda(), bold_downsamp=dec).cpu().numpy()
+    assert got.shape == want.shape
+    assert np.abs(got - want).max() <= 1e-7 * np.abs(want).max(), np.abs(got - want).max() / np.abs(want).max()
+
+
+def test_bold_chunking_is_exact(cuda):
+    T, C = 9_000, 5
+    E = torch.from_numpy(_e_like(T, C, 7)).cuda()
+    one = wsg.sim_bold(E, bold_downsamp=1000)
+    bs = wsg.BoldStream(C, T, dec=1000)
+    for a, b in ((0, 17), (17, 2000), (2000, 2001), (2001, 5555), (5555, T)):
+        bs.feed(E[a:b].contiguous())
+    assert torch.equal(one, bs.finish())
+    # node-major ring-slot input (e_ld) gives the same
+    nm = E.t().contiguous()
+    bs2 = wsg.BoldStream(C, T, dec=1000)
+    bs2.feed(nm, T, e_ld=T)
+    assert torch.equal(one, bs2.finish())
+
+
+def test_fc_metrics_vs_oracle(cuda):
+    rng = np.random.default_rng(3)
+    B, N, M = 5, 90, 298
+    bold = rng.standard_normal((M, B, N)).cumsum(0) + rng.standard_normal((M, B, 1))
+    emp = {s: datasets.load_empfc(s) for s in datasets.STATES}
+    fc, met, extra = wsg.fc_metrics(torch.from_numpy(bold).cuda(), B, N, np.stack(list(emp.values())),
+                                    want_fc=True)
+    fc, met, extra = fc.cpu().numpy(), met.cpu().numpy(), extra.cpu().numpy()
+    for b in range(B):
+        sfc = np.corrcoef(bold[:, b, :].T)
+        np.testing.assert_allclose(fc[b], sfc, rtol=0, atol=1e-12)
+        for k, s in enumerate(emp):
+            np.testing.assert_allclose(met[b, k], osg.get_all_metrics(sfc, emp[s], 1), rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(extra[b, 0], np.mean(sfc), rtol=1e-12)
+        np.testing.assert_allclose(extra[b, 1:], osg.kuramoto(bold[:, b, :]), rtol=1e-9)
+
+
+def test_gof_vs_reference_utils_golden(cuda):
+    """fc_in mode against the reference's own utils.get_all_metrics outputs."""
+    inp = inputs()
+    gu = np.load(os.path.join(G, "golden_utils.npz"))
+    emps = np.stack([datasets.load_empfc(s) for s in ("W", "N1", "N2", "N3")])
+    fcs = np.stack(inp["fcs"] + [emps[0], emps[3]])
+    _, met, _ = wsg.fc_metrics(fc_in=torch.from_numpy(fcs).cuda(), empfc=emps)
+    np.testing.assert_allclose(met.cpu().numpy(), gu["metrics"], rtol=1e-9, atol=1e-12)
+
+
+def test_kuramoto_vs_reference_utils_golden(cuda):
+    inp = inputs()
+    gu = np.load(os.path.join(G, "golden_utils.npz"))
+    for i, k in enumerate(inp["kur"]):
+        M, N = k.shape
+        _, _, extra = wsg.fc_metrics(torch.from_numpy(k).cuda(), 1, N, None)
+        np.testing.assert_allclose(extra[0, 1:].cpu().numpy(), gu["kuramoto"][i], rtol=1e-9)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_welch_vs_oracle(cuda, dtype):
+    B, N, T = 3, 7, 20_000
+    E = _e_like(T, B * N, 11).reshape(T, B, N)
+    Et = torch.from_numpy(E).to("cuda", dtype)
+    peak, psd = wsg.welch_peak(Et, want_psd=True)
+    Eh = Et.double().cpu().numpy()
+    for b in range(B):
+        f, P = osg.welch_psd(Eh[:, b, :].T, 500.0, 4000)
+        mp = P.mean(axis=0)
+        rt = 1e-9 if dtype == torch.float64 else 2e-4
+        np.testing.assert_allclose(psd[b].cpu().numpy(), mp, rtol=rt, atol=rt * mp.max())
+        assert peak[b].item() == osg.welch_peak(Eh[:, b, :])
+
+
+def test_welch_golden_full_length(cuda):
+    """300,000-sample input of the SciPy golden: node-mean PSD and peak."""
+    inp = inputs()
+    gs = np.load(os.path.join(G, "golden_scipy.npz"))
+    E = torch.from_numpy(inp["e_t"]).cuda()[:, None, :]  # [T][1][3]
+    peak, psd = wsg.welch_peak(E, want_psd=True)
+    mp = gs["welch_P"].mean(axis=0)
+    np.testing.assert_allclose(psd[0].cpu().numpy(), mp, rtol=1e-9, atol=1e-9 * mp.max())
+    assert peak[0].item() == gs["welch_f"][np.argmax(mp)]
+
+
+def test_pipeline_short_schedule_vs_oracle(cuda, sc90):
+    """run_sweep end to end (fp64) vs the oracle's run() + sim_metrics per simulation."""
+    from nremmodfc_amd.model import Schedule, driver_params, sim_keys
+    from nremmodfc_amd.pipeline import run_sweep
+    sch = Schedule(n_trans1=200, n_trans2=2000, n_sim=200_000)  # T = 10,000 samples
+    G = np.array([0.16, 0.10, 0.22, 0.16, 0.30])
+    S = np.array([7.68, 7.50, 7.80, 7.88, 7.68])
+    keys = sim_keys([0, 1, 2, 3, 4], [0, 5, 9, 11, 3])
+    emp = {s: datasets.load_empfc(s) for s in datasets.STATES}
+    res = run_sweep(sc90, G, S, keys, emp, sch, precision="f64", want_fc=True, want_bold=True)
+    p = driver_params()
+    ob = oracle.OracleBatch(sc90, G, S, keys, p)
+    ob.integrate(sch.n_trans1, 0.05)
+    ob.integrate(sch.n_trans2, 1.0)
+    rec = ob.integrate(sch.n_sim, 2.0, 20)  # [B][T][N]
+    cols = res.columns()
+    for b in range(len(keys)):
+        want, wbold, wfc = osg.sim_metrics(rec[b], emp)
+        scale = np.abs(wbold).max()
+        assert np.abs(res.bold[:, b, :] - wbold).max() <= 1e-7 * scale
+        assert np.abs(res.fc[b] - wfc).max() <= 1e-6
+        for name, v in want.items():
+            if name == "peakfreq":
+                assert cols[name][b] == v, (name, cols[name][b], v)
+            else:
+                np.testing.assert_allclose(cols[name][b], v, rtol=1e-6, atol=1e-8, err_msg=name)
