@@ -144,12 +144,16 @@ int wc_hilbert_phase(int64_t C, int M, const double* x, double* phasor, void* wo
 /* Per simulation b of bold [M][B][N] (the filtered, decimated BOLD; or, with
  * bold == NULL, of the given fc_in [B][N][N]):
  *   fc_out [B][N][N]  np.corrcoef(BOLD.T)                (may be NULL)
- *   metrics [B][K][4] utils.get_all_metrics(sFC, empfc[k], 1) = corr, euc, ssim, new_metric
+ *   metrics [B][K][4] utils.get_all_metrics(sFC, empfc[k], data_range) = corr, euc, ssim, new_metric
  *   extra [B][3]      np.mean(sFC), kuramoto sync, meta (sync/meta 0 if phasor NULL)
  * 7 <= N <= 96. */
 int wc_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, const double* empfc,
-                  int K, const double* phasor, double* fc_out, double* metrics, double* extra,
-                  void* stream);
+                  int K, double data_range, const double* phasor, double* fc_out, double* metrics,
+                  double* extra, void* stream);
+
+/* utils.kuramoto (utils.py:34-40) from unit phasors [M][B][N][2] (wc_hilbert_phase):
+ * out [B][2] = (mean_t R(t), std_t R(t)), R(t) = |mean_n exp(i theta_n(t))|. */
+int wc_kuramoto(int B, int N, int M, const double* phasor, double* out, void* stream);
 
 /* ------------------------------------------------------------------------
  * Welch peak frequency (whole_sweep_both.py:90-95): signal.welch(E_t.T, fs,

@@ -1,0 +1,89 @@
+"""Hierarchical module analysis of FC (integration / segregation), drop-in for HMA.py.
+
+Same algorithm and call surface as the reference's HMA.py:30-203 (Wang et al.
+2019, 2021; adapted by C. Coronel): eigenmode-based hierarchical modules of the
+positive part of FC -> Clus_num / Clus_size per level -> integration Hin and
+segregation Hse, global and nodal.  The reference builds the module tree with
+exec/eval of generated variable names; here the tree is plain lists, with the
+same ordering (level k+1 lists, for every module of level k in order, its
+negative part then its positive part; empty modules dropped).
+
+Runs on the host (numpy SVD of one N x N matrix per simulation): it is the
+per-simulation epilogue of run_many_seeds.py:130-133,
+three 90x90 SVDs per simulation.  Like the reference, every function clips the
+caller's FC in place (FC[FC < 0] = 0, HMA.py:55) -- run_many_seeds saves that
+clipped sFC.
+"""
+import numpy as np
+
+
+def _positive_sym(FC):
+    FC[FC < 0] = 0          # in place, as the reference (HMA.py:55, :123, :178)
+    return (FC + FC.T) / 2
+
+
+def Functional_HP(FC):
+    """Hierarchical modules (HMA.py:30-103) -> [Clus_num, Clus_size, H_all]."""
+    N = FC.shape[0]
+    F = _positive_sym(FC)
+    u, s, v = np.linalg.svd(F)
+    H1 = [np.argwhere(u[:, 1] < 0)[:, 0], np.argwhere(u[:, 1] >= 0)[:, 0]]
+    H_all = [H1]
+    Clus_num = [1]
+    Clus_size = [[N]]
+    prev_named = H1  # level-k modules in index order (neg, pos per parent)
+    for mode in range(1, N - 1):
+        x = np.argwhere(u[:, mode + 1] >= 0)[:, 0]
+        y = np.argwhere(u[:, mode + 1] < 0)[:, 0]
+        H = prev_named[:2 * Clus_num[mode - 1]]
+        idx = np.array([len(h) for h in H])
+        H = [H[f] for f in range(len(idx)) if idx[f] != 0]
+        idx = [idx[f] for f in range(len(idx)) if idx[f] != 0]
+        Clus_size.append(idx)
+        Clus_num.append(len(H))
+        level, named = [], []
+        for h in H:
+            pos = np.intersect1d(h, x)
+            neg = np.intersect1d(h, y)
+            level += [pos, neg]   # the reference appends H_{j+2} (pos) then H_{j+1} (neg)
+            named += [neg, pos]   # ... and the next level reads them by index: neg first
+        H_all.append(level)
+        prev_named = named
+    return [Clus_num, Clus_size, H_all]
+
+
+def _hf(FC, Clus_num, Clus_size):
+    N = FC.shape[0]
+    F = _positive_sym(FC)
+    u, s, v = np.linalg.svd(F)
+    s[s < 0] = 0
+    s = s ** 2
+    p = np.zeros(N - 1)
+    for i in range(0, len(Clus_num) - 1):
+        p[i] = np.sum(np.abs(np.array(Clus_size[i]) - N / Clus_num[i])) / N
+    HF = s[0:(N - 1)] * np.array(Clus_num) * (1 - p)
+    return HF, u, N
+
+
+def Balance(FC, Clus_num, Clus_size):
+    """Integration and segregation components (HMA.py:107-151) -> [Hin, Hse]."""
+    HF, _, N = _hf(FC, Clus_num, Clus_size)
+    return [np.sum(HF[0]) / N ** 2, np.sum(HF[1:(N - 1)]) / N ** 2]
+
+
+def nodal_measures(FC, Clus_num, Clus_size):
+    """Nodal integration / segregation (HMA.py:155-203) -> [Hin_nodal, Hse_nodal]."""
+    HF, u, N = _hf(FC, Clus_num, Clus_size)
+    Hin_nodal = HF[0] / N * u[:, 0] ** 2
+    Hse_nodal = np.zeros(N)
+    for i in range(1, N - 1):
+        Hse_nodal += HF[i] / N * u[:, i] ** 2
+    return [Hin_nodal, Hse_nodal]
+
+
+def integration_segregation(sFC):
+    """run_many_seeds.py:130-136 for one simulation: the dict it pickles."""
+    cn, cs, _ = Functional_HP(sFC)
+    hin, hse = Balance(sFC, cn, cs)
+    hin_n, hse_n = nodal_measures(sFC, cn, cs)
+    return {"Hin_sim": hin, "Hse_sim": hse, "Hin_node_sim": hin_n, "Hse_node_sim": hse_n, "sFC": sFC}

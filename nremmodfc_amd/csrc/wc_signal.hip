@@ -331,6 +331,42 @@ __device__ double block_sum(double v, double* red) {
     return s;
 }
 
+// Kuramoto order parameter of B groups of N columns: R(t) = |mean_n phasor|,
+// out[b] = (mean_t R, std_t R) (utils.py:37-39, np.std ddof 0)
+__global__ void __launch_bounds__(256) kuramoto_kernel(int B, int N, int M, const double* __restrict__ ph,
+                                                       double* __restrict__ out) {
+    __shared__ double red[8];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int64_t C = (int64_t)B * N;
+    double r1 = 0;
+    for (int t = tid; t < M; t += blockDim.x) {
+        double cr = 0, ci = 0;
+        const double* p = ph + ((int64_t)t * C + (int64_t)b * N) * 2;
+        for (int n = 0; n < N; ++n) {
+            cr += p[2 * n];
+            ci += p[2 * n + 1];
+        }
+        r1 += sqrt((cr / N) * (cr / N) + (ci / N) * (ci / N));
+    }
+    const double sync = block_sum(r1, red) / M;
+    double r2 = 0;
+    for (int t = tid; t < M; t += blockDim.x) {
+        double cr = 0, ci = 0;
+        const double* p = ph + ((int64_t)t * C + (int64_t)b * N) * 2;
+        for (int n = 0; n < N; ++n) {
+            cr += p[2 * n];
+            ci += p[2 * n + 1];
+        }
+        const double R = sqrt((cr / N) * (cr / N) + (ci / N) * (ci / N));
+        r2 += (R - sync) * (R - sync);
+    }
+    const double meta = sqrt(block_sum(r2, red) / M);
+    if (tid == 0) {
+        out[2 * b] = sync;
+        out[2 * b + 1] = meta;
+    }
+}
+
 struct FcArgs {
     int B, N, M, K;
     const double* bold;   // [M][B][N] band-passed, decimated BOLD (NULL: take fc_in)
@@ -340,6 +376,7 @@ struct FcArgs {
     double* fc;           // [B][N][N] (may be NULL)
     double* metrics;      // [B][K][4]: corr, euc, ssim, new_metric
     double* extra;        // [B][3]: mean(FC), sync, meta
+    double data_range;    // SSIM data range (utils.py:48 passes 1)
 };
 
 // LDS: fc[N*N] | emp[N*N] (also the time-chunk staging area before emp is loaded) | red[8]
@@ -473,7 +510,8 @@ __global__ void __launch_bounds__(kFcThreads) fc_metrics_kernel(const FcArgs a) 
         if (band < nbands) {
             const int j = jcol + 3;
             const int r0 = 3 + (P * band) / nbands, r1 = 3 + (P * (band + 1)) / nbands;
-            const double C1 = 0.01 * 0.01, C2 = 0.03 * 0.03, cov_norm = 49.0 / 48.0;
+            const double C1 = (0.01 * a.data_range) * (0.01 * a.data_range),
+                         C2 = (0.03 * a.data_range) * (0.03 * a.data_range), cov_norm = 49.0 / 48.0;
             for (int i = r0; i < r1; ++i) {
                 double vx = 0, vy = 0, vxx = 0, vyy = 0, vxy = 0;
                 for (int di = -3; di <= 3; ++di) {
@@ -730,13 +768,21 @@ int wc_hilbert_phase(int64_t C, int M, const double* x, double* phasor, void* wo
     return wc_hip_check("wc_hilbert_phase");
 }
 
+int wc_kuramoto(int B, int N, int M, const double* phasor, double* out, void* stream) {
+    wc_clear_err();
+    if (B <= 0 || N <= 0 || M <= 0 || !phasor || !out) return wc_set_err(WC_EINVAL, "wc_kuramoto: bad arguments");
+    hipLaunchKernelGGL(kuramoto_kernel, dim3(B), dim3(256), 0, static_cast<hipStream_t>(stream), B, N, M, phasor, out);
+    return wc_hip_check("wc_kuramoto");
+}
+
 int wc_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, const double* empfc, int K,
-                  const double* phasor, double* fc_out, double* metrics, double* extra, void* stream) {
+                  double data_range, const double* phasor, double* fc_out, double* metrics, double* extra,
+                  void* stream) {
     wc_clear_err();
     if (B <= 0 || N < 7 || N > 96 || M < 2 || K < 0 || (!bold && !fc_in) || !extra ||
         (K > 0 && (!empfc || !metrics)))
         return wc_set_err(WC_EINVAL, "wc_fc_metrics: bad arguments (7 <= N <= 96)");
-    FcArgs a{B, N, M, K, bold, fc_in, empfc, phasor, fc_out, metrics, extra};
+    FcArgs a{B, N, M, K, bold, fc_in, empfc, phasor, fc_out, metrics, extra, data_range};
     const size_t lds = (size_t)(2 * N * N + 8 + N) * sizeof(double);
     hipError_t e = hipFuncSetAttribute((const void*)fc_metrics_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);

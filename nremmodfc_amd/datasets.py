@@ -27,6 +27,8 @@ def load_empfc(state):
 
 
 def load_map(name, n=90):
-    """Map normalised to mean 1 (whole_sweep_both_maps.py:47-57); HOMO = ones."""
-    m = np.ones(n) if name == "HOMO" else np.load(os.path.join(DATA, name + ".npy")).astype(np.float64)
-    return m / m.mean()
+    """Map normalised to mean 1 (whole_sweep_both_maps.py:47-57); HOMO = ones.
+    The division happens in the file's dtype (float32 for the VAChT maps), as
+    the reference does, and only then is widened to float64."""
+    m = np.ones(n) if name == "HOMO" else np.load(os.path.join(DATA, name + ".npy"))
+    return (m / m.mean()).astype(np.float64)

@@ -83,7 +83,7 @@ def hilbert_phase(x):
     return ph
 
 
-def fc_metrics(bold=None, B=None, N=None, empfc=None, fc_in=None, kuramoto=True, want_fc=False):
+def fc_metrics(bold=None, B=None, N=None, empfc=None, fc_in=None, kuramoto=True, want_fc=False, data_range=1.0):
     """Per simulation: FC (np.corrcoef(BOLD.T)), get_all_metrics vs each empfc,
     mean(FC), Kuramoto sync/meta.
 
@@ -107,9 +107,20 @@ def fc_metrics(bold=None, B=None, N=None, empfc=None, fc_in=None, kuramoto=True,
     fc = torch.empty((B, N, N), dtype=torch.float64, device=dev) if want_fc else None
     ph = hilbert_phase(bold) if kuramoto else None
     rc = L.wc_fc_metrics(B, N, M, _lib.ptr(bold) if bold is not None else None, _lib.ptr(fc_in), _lib.ptr(emp), K,
-                         _lib.ptr(ph), _lib.ptr(fc), _lib.ptr(metrics), _lib.ptr(extra), _lib.stream_handle())
+                         float(data_range), _lib.ptr(ph), _lib.ptr(fc), _lib.ptr(metrics), _lib.ptr(extra), _lib.stream_handle())
     _lib.check(rc, "wc_fc_metrics")
     return fc, metrics[:, :K], extra
+
+
+def kuramoto(x, B=1, N=None):
+    """utils.kuramoto of x [M][B*N] (or [M][N]) fp64 on the device -> [B][2] (sync, meta)."""
+    M = x.shape[0]
+    x = x.reshape(M, -1).contiguous()
+    N = x.shape[1] // B if N is None else N
+    ph = hilbert_phase(x)
+    out = torch.empty((B, 2), dtype=torch.float64, device=x.device)
+    _lib.check(_lib.lib().wc_kuramoto(B, N, M, _lib.ptr(ph), _lib.ptr(out), _lib.stream_handle()), "wc_kuramoto")
+    return out
 
 
 class WelchAccumulator:

@@ -1,0 +1,274 @@
+"""Sweep drivers: whole_sweep_both.py, whole_sweep_both_maps.py, run_many_seeds.py.
+
+The reference runs each driver as a 64-task SLURM array of single-threaded
+processes (`sim % threads == rank`, whole_sweep_both.py:63-64) that append one
+TSV line per simulation (:112-116); a human then concatenates the per-rank
+files into the comma-separated `output/*.txt` that heatmaps.py reads.  Here one
+process per GPU (torchrun / the same SLURM variables) takes its shard of the
+same `itertools.product` list, runs it through the streamed GPU pipeline in
+large batches, appends the same TSV lines (resumable: simulations already in
+the rank's file are skipped), and rank 0 gathers every row over RCCL (one
+all-gather of a float64 table) and writes the collapsed CSV itself.
+
+  python -m nremmodfc_amd.sweep homo      [--seeds 50 --seed0 0] [--grid shipped|script]
+  python -m nremmodfc_amd.sweep maps      --map-ids 1 1  [--seeds 25 --seed0 25]
+  python -m nremmodfc_amd.sweep many      --modality homo|map|shuf
+  torchrun --nproc-per-node 8 -m nremmodfc_amd.sweep homo ...
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import itertools
+import os
+import pickle
+from typing import List, Optional
+
+import numpy as np
+
+from . import datasets
+
+STATES = datasets.STATES
+METRIC_COLS = (["ssim" + s for s in STATES] + ["corr" + s for s in STATES] + ["e" + s for s in STATES]
+               + ["sync", "meta", "mean", "peakfreq"])
+HEADER = ["rank", "seed", "delta_G", "delta_sigma"] + METRIC_COLS  # whole_sweep_both.py:115
+BASE_G, BASE_SIGMA = 0.16, 7.68  # whole_sweep_both.py:30 ("W optimal")
+
+# run_many_seeds.py:34-47 -- (G, delta_G, sigmaE, delta_sigmaE) per state, from heatmaps.py
+OPTIMALS = {
+    "homo": {"W": (0.16, 0.0, 7.68, 0.0), "N1": (0.16, 0.04, 7.68, 0.0), "N2": (0.16, 0.0, 7.68, 0.0),
+             "N3": (0.16, -0.04, 7.68, 0.04)},
+    "map": {"W": (0.16, -0.02, 7.68, -0.02), "N1": (0.16, 0.18, 7.68, -0.02), "N2": (0.16, 0.02, 7.68, -0.04),
+            "N3": (0.16, 0.02, 7.68, -0.12)},
+    "shuf": {"W": (0.16, 0.0, 7.68, 0.0), "N1": (0.16, 0.0, 7.68, 0.04), "N2": (0.16, 0.0, 7.68, 0.0),
+             "N3": (0.16, 0.0, 7.68, -0.04)},
+}
+MODALITY_MAPS = {"homo": (0, 0), "map": (1, 1), "shuf": (2, 2)}
+
+
+@dataclasses.dataclass
+class Sim:
+    index: int              # position in the reference's product list
+    seed: int
+    dG: float
+    dsigma: float
+    G: np.ndarray           # (N,)
+    sigma: np.ndarray       # (N,)
+    stream: int             # Philox stream id (grid cell / state index): key = (seed, stream)
+    state: Optional[str] = None
+
+
+def _grids(kind):
+    if kind == "script":   # the values written in whole_sweep_both.py:57-58
+        return np.linspace(-0.1, 0.5, 20, endpoint=False), np.linspace(-1, 1, 20, endpoint=False)
+    # the grid the shipped outputs were produced on (whole_sweep_both_maps.py:92-93; SURVEY.md 0, gotcha 5)
+    return np.linspace(-0.1, 0.3, 20, endpoint=False), np.linspace(-0.2, 0.2, 20, endpoint=False)
+
+
+def homogeneous(n_iterations=50, n_init=0, grid="shipped", n=90) -> List[Sim]:
+    """whole_sweep_both.py:57-72: G = 0.16 + dG, sigmaE = 7.68 + dsigma on every node."""
+    return maps(0, 0, n_iterations, n_init, grid, n)
+
+
+def maps(map_id1=1, map_id2=1, n_iterations=25, n_init=25, grid="shipped", n=90) -> List[Sim]:
+    """whole_sweep_both_maps.py:92-108: G_i = 0.16 + dG*ach_i, sigmaE_i = 7.68 + dsigma*na_i
+    (maps normalised to mean 1; id 0 homogeneous, 1 real, 2 hemisphere-symmetric shuffle)."""
+    ach = datasets.load_map(datasets.MAPNAMES_ACH[map_id1], n)
+    na = datasets.load_map(datasets.MAPNAMES_NA[map_id2], n)
+    dGs, dSs = _grids(grid)
+    seeds = range(n_init, n_init + n_iterations)
+    out = []
+    for i, (seed, a, b) in enumerate(itertools.product(seeds, range(len(dGs)), range(len(dSs)))):
+        dG, dS = dGs[a], dSs[b]
+        out.append(Sim(i, seed, dG, dS, BASE_G + dG * ach, BASE_SIGMA + dS * na, a * len(dSs) + b))
+    return out
+
+
+def many_seeds(modality="map", n_iterations=50, n_init=0, n=90) -> List[Sim]:
+    """run_many_seeds.py:105-117: product(seeds, states) at each state's optimum."""
+    m1, m2 = MODALITY_MAPS[modality]
+    ach = datasets.load_map(datasets.MAPNAMES_ACH[m1], n)
+    na = datasets.load_map(datasets.MAPNAMES_NA[m2], n)
+    out = []
+    seeds = range(n_init, n_init + n_iterations)
+    for i, (seed, state) in enumerate(itertools.product(seeds, STATES)):
+        G, dG, s, dS = OPTIMALS[modality][state]
+        out.append(Sim(i, seed, dG, dS, G + ach * dG, s + na * dS, 1000 + STATES.index(state), state))
+    return out
+
+
+def shard(sims: List[Sim], rank: int, world: int) -> List[Sim]:
+    """The reference's round-robin: simulation i belongs to rank i % world."""
+    return [s for s in sims if s.index % world == rank]
+
+
+def format_row(rank, sim: Sim, vals: dict) -> str:
+    """One TSV line exactly as whole_sweep_both.py:116 writes it."""
+    parts = [str(rank), str(sim.seed), f"{sim.dG:.4f}", f"{sim.dsigma:.4f}"] + [f"{vals[c]:.4f}" for c in METRIC_COLS]
+    return "\t".join(parts) + "\n"
+
+
+def done_keys(path):
+    """(seed, delta_G, delta_sigma) already in a rank file (resume after a crash)."""
+    if not os.path.exists(path):
+        return set()
+    keys = set()
+    with open(path) as f:
+        next(f, None)
+        for line in f:
+            p = line.rstrip("\n").split("\t")
+            if len(p) == len(HEADER):
+                keys.add((int(p[1]), p[2], p[3]))
+    return keys
+
+
+def append_rows(path, rank, sims, results):
+    new = not os.path.isfile(path)
+    with open(path, "a") as f:
+        if new:
+            f.write("\t".join(HEADER) + "\n")
+        for s, r in zip(sims, results):
+            f.write(format_row(rank, s, r))
+
+
+def collapse(paths, out_csv):
+    """Concatenate per-rank TSV files into the comma-separated table heatmaps.py reads."""
+    import pandas as pd
+    df = pd.concat([pd.read_csv(p, sep="\t") for p in paths if os.path.exists(p)], ignore_index=True)
+    df.to_csv(out_csv, index=False)
+    return df
+
+
+def run_sims(sims: List[Sim], sc, empfcs, schedule=None, precision="f32", batch=20_000, device="cuda",
+             want_fc=False, progress=None):
+    """Run simulations through the GPU pipeline in batches -> (list of metric dicts, FCs or None)."""
+    from .model import sim_keys
+    from .pipeline import run_sweep
+    rows, fcs = [], []
+    for b0 in range(0, len(sims), batch):
+        part = sims[b0:b0 + batch]
+        G = np.stack([s.G for s in part])
+        S = np.stack([s.sigma for s in part])
+        keys = sim_keys([s.seed for s in part], [s.stream for s in part])
+        res = run_sweep(sc, G, S, keys, empfcs, schedule, precision=precision, want_fc=want_fc, device=device,
+                        progress=progress)
+        cols = res.columns()
+        rows += [{c: float(cols[c][i]) for c in METRIC_COLS} for i in range(len(part))]
+        if want_fc:
+            fcs += list(res.fc)
+    return rows, (fcs if want_fc else None)
+
+
+def rows_table(rank, sims, rows):
+    """float64 table [n][4 + 16]: rank, index, seed, stream, metrics."""
+    t = np.zeros((len(sims), 4 + len(METRIC_COLS)))
+    for i, (s, r) in enumerate(zip(sims, rows)):
+        t[i, :4] = (rank, s.index, s.seed, s.stream)
+        t[i, 4:] = [r[c] for c in METRIC_COLS]
+    return t
+
+
+def gather_table(table, dist, device):
+    """All ranks' row tables on every rank (one all-gather over RCCL/gloo), sorted by index."""
+    import torch
+    n = torch.tensor([table.shape[0]], device=device)
+    world = dist.get_world_size()
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    m = int(max(x.item() for x in ns))
+    buf = torch.full((m, table.shape[1]), float("nan"), dtype=torch.float64, device=device)
+    buf[:table.shape[0]] = torch.as_tensor(table, dtype=torch.float64, device=device)
+    out = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf)
+    full = torch.cat([o[:int(k.item())] for o, k in zip(out, ns)]).cpu().numpy()
+    return full[np.argsort(full[:, 1], kind="stable")]
+
+
+def _rank_world():
+    if "WORLD_SIZE" in os.environ:
+        return int(os.environ.get("RANK", 0)), int(os.environ["WORLD_SIZE"]), int(os.environ.get("LOCAL_RANK", 0))
+    if "SLURM_ARRAY_TASK_ID" in os.environ:  # the reference's launcher (whole_sweep_both.py:23-24)
+        return int(os.environ["SLURM_ARRAY_TASK_ID"]), int(os.environ["SLURM_ARRAY_TASK_MAX"]) + 1, 0
+    return 0, 1, 0
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("kind", choices=("homo", "maps", "many"))
+    ap.add_argument("--seeds", type=int, default=None)
+    ap.add_argument("--seed0", type=int, default=None)
+    ap.add_argument("--grid", default="shipped", choices=("shipped", "script"))
+    ap.add_argument("--map-ids", type=int, nargs=2, default=(1, 1))
+    ap.add_argument("--modality", default="map", choices=("homo", "map", "shuf"))
+    ap.add_argument("--out", default="output")
+    ap.add_argument("--tag", default=None)
+    ap.add_argument("--precision", default="f32", choices=("f32", "f64"))
+    ap.add_argument("--batch", type=int, default=20_000)
+    ap.add_argument("--short", action="store_true", help="short schedule (smoke runs): 0.02/0.2/20 s")
+    ap.add_argument("--limit", type=int, default=None, help="only the first LIMIT simulations of the list")
+    args = ap.parse_args(argv)
+
+    import torch
+    from .model import Schedule
+    rank, world, local = _rank_world()
+    dist = None
+    device = f"cuda:{local}"
+    if world > 1 and "WORLD_SIZE" in os.environ:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    os.makedirs(os.path.join(args.out, "temp"), exist_ok=True)
+    if args.kind == "homo":
+        sims = homogeneous(args.seeds or 50, args.seed0 or 0, args.grid)
+        tag = args.tag or f"sweep_delta_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_0_0"
+    elif args.kind == "maps":
+        m1, m2 = args.map_ids
+        sims = maps(m1, m2, args.seeds or 25, 25 if args.seed0 is None else args.seed0, args.grid)
+        name = "deltaSHUFFLED" if (m1, m2) == (2, 2) else "deltamaps"
+        tag = args.tag or f"sweep_{name}_from_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_{m1}_{m2}"
+    else:
+        sims = many_seeds(args.modality, args.seeds or 50, args.seed0 or 0)
+        tag = args.tag or f"run_50seeds_output_{args.modality}"
+    if args.limit:
+        sims = sims[:args.limit]
+    sched = Schedule(n_trans1=200, n_trans2=2000, n_sim=200_000) if args.short else Schedule()
+    empfcs = {s: datasets.load_empfc(s) for s in STATES}
+    sc = datasets.load_sc()
+    mine = shard(sims, rank, world)
+
+    if args.kind == "many":
+        from . import HMA
+        rows, fcs = run_sims(mine, sc, empfcs, sched, args.precision, args.batch, device, want_fc=True)
+        save = {(s.seed, s.state): HMA.integration_segregation(fc.copy()) for s, fc in zip(mine, fcs)}
+        with open(os.path.join(args.out, "temp", f"{tag}_rank{rank}.pickle"), "wb") as f:
+            pickle.dump(save, f)
+        if dist:
+            parts = [None] * world
+            dist.all_gather_object(parts, save)
+        else:
+            parts = [save]
+        if rank == 0:
+            merged = {k: v for p in parts for k, v in p.items()}
+            merged["metainfo"] = {st: sum(1 for k in merged if k != "metainfo" and k[1] == st) for st in STATES}
+            with open(os.path.join(args.out, f"{tag}.pickle"), "wb") as f:
+                pickle.dump(merged, f)
+    else:
+        path = os.path.join(args.out, "temp", f"{tag}_rank{rank}")
+        have = done_keys(path)
+        todo = [s for s in mine if (s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") not in have]
+        rows, _ = run_sims(todo, sc, empfcs, sched, args.precision, args.batch, device)
+        append_rows(path, rank, todo, rows)
+        table = rows_table(rank, todo, rows)
+        if dist:
+            table = gather_table(table, dist, torch.device(device))
+        if rank == 0:
+            paths = [os.path.join(args.out, "temp", f"{tag}_rank{r}") for r in range(world)]
+            collapse(paths, os.path.join(args.out, f"{tag}.txt"))
+            np.save(os.path.join(args.out, f"{tag}_rows.npy"), table)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

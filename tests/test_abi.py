@@ -52,5 +52,6 @@ def test_invalid_arguments_fail_loudly():
     cfg = _lib.WCBoldCfgC()
     cfg.dec, cfg.neq, cfg.n_total = 1000, 2000, 2010  # fewer than neq + 16 samples
     assert L.wc_bold_init(ctypes.byref(cfg), 10, ctypes.c_void_p(16), None) == -1
-    assert L.wc_fc_metrics(1, 200, 298, None, None, None, 0, None, None, None, None, None) == -1
+    assert L.wc_fc_metrics(1, 200, 298, None, None, None, 0, 1.0, None, None, None, None, None) == -1
+    assert L.wc_kuramoto(0, 90, 298, None, None, None) == -1
     assert L.wc_welch_bins() == 2001

@@ -1,0 +1,81 @@
+"""Drop-in module facades (netwWilsonCowanPlastic, utils) used the reference's way.
+
+Tolerances: wc.run() fp64 vs the oracle 1e-9 (same as test_sde_gpu); simBOLD
+1e-7 relative (filtfilt conditioning, see test_signal_gpu); utils against the
+reference's own utils.py outputs (golden_utils.npz) rtol 1e-9.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import oracle.sigchain as osg
+from nremmodfc_amd import datasets
+from tests.golden.make_golden import inputs
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_utils_get_all_metrics_golden(cuda):
+    from nremmodfc_amd import utils
+    gu = np.load(os.path.join(G, "golden_utils.npz"))
+    emps = [datasets.load_empfc(s) for s in datasets.STATES]
+    fcs = inputs()["fcs"] + [emps[0], emps[3]]
+    for i, fc in enumerate(fcs):
+        for j, e in enumerate(emps):
+            got = utils.get_all_metrics(fc, e, data_range=1)
+            np.testing.assert_allclose(got, gu["metrics"][i, j], rtol=1e-9, atol=1e-12)
+
+
+def test_utils_kuramoto_golden(cuda):
+    from nremmodfc_amd import utils
+    gu = np.load(os.path.join(G, "golden_utils.npz"))
+    for i, k in enumerate(inputs()["kur"]):
+        np.testing.assert_allclose(utils.kuramoto(k), gu["kuramoto"][i], rtol=1e-9)
+
+
+def test_wc_run_like_reference_driver(cuda, sc90):
+    """whole_sweep_both.py:39-78 style: set module globals, recompile, run, simBOLD."""
+    from nremmodfc_amd import netwWilsonCowanPlastic as wc
+    from nremmodfc_amd.model import driver_params, sim_keys
+    wc.P, wc.rhoE, wc.CM = 0.4, 0.18, sc90
+    wc.precision = "f64"
+    wc.tTrans1, wc.tTrans2, tstop = 0.02, 0.2, 2.0
+    wc.timeTrans1 = np.arange(0, wc.tTrans1, wc.dtSim)
+    wc.timeTrans2 = np.arange(0, wc.tTrans2, wc.dtSim)
+    wc.tstop = tstop
+    wc.timeSim = np.arange(0, tstop, wc.dtSim)
+    wc.time = np.arange(0, tstop, wc.dt)
+    wc.G, wc.sigmaE, wc.sid = 0.16, 7.68, 3
+    wc.run.recompile()
+    tray = wc.run()
+    assert tray.shape == (len(wc.time), 3, 90) and tray.dtype == np.float64
+
+    ob = oracle.OracleBatch(sc90, 0.16, 7.68, sim_keys([3], [0]), driver_params())
+    ob.integrate(len(wc.timeTrans1), 0.05)
+    ob.integrate(len(wc.timeTrans2), 1.0)
+    rec = ob.integrate(len(wc.timeSim), 2.0, wc.downsamp)[0]
+    np.testing.assert_allclose(tray[:, 0, :], rec, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(tray[-1, 2, :], ob.A[0], rtol=0, atol=1e-3)  # a_ie: last record is <20 steps before the end
+    assert np.isfinite(tray).all()
+
+    E = np.tile(tray[:, 0, :], (7, 1))  # 7000 samples: past the 2000-sample BOLD transient
+    bold = wc.simBOLD(E, nnodes=90)
+    want = osg.sim_bold(E, bold_downsamp=1000)
+    assert bold.shape == want.shape
+    assert np.abs(bold - want).max() <= 1e-7 * np.abs(want).max()
+
+
+def test_wc_run_checks_globals(cuda):
+    from nremmodfc_amd import netwWilsonCowanPlastic as wc
+    n = wc.N
+    wc.N = n + 1
+    try:
+        with pytest.raises(ValueError):
+            wc.run()
+    finally:
+        wc.N = n
+    with pytest.raises(NotImplementedError):
+        wc.wilsonCowan()

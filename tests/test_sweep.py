@@ -1,0 +1,146 @@
+"""Sweep drivers (nremmodfc_amd/sweep.py) against the reference drivers' lists,
+formats and the shipped output tables (tests/golden/shipped_*_head.csv are the
+first rows of /root/reference/output/*.txt, copied by make_golden.py)."""
+import itertools
+import os
+
+import numpy as np
+import pytest
+
+from nremmodfc_amd import datasets, sweep
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_homo_list_matches_reference_product():
+    sims = sweep.homogeneous(n_iterations=3, n_init=5)
+    dG = np.linspace(-0.1, 0.3, 20, endpoint=False)
+    dS = np.linspace(-0.2, 0.2, 20, endpoint=False)
+    ref = list(itertools.product(np.arange(5, 8), dG, dS))  # whole_sweep_both_maps.py:92-96
+    assert len(sims) == len(ref) == 1200
+    for s, (seed, g, d) in zip(sims, ref):
+        assert (s.seed, s.dG, s.dsigma) == (seed, g, d)
+        np.testing.assert_array_equal(s.G, 0.16 + g * np.ones(90))
+        np.testing.assert_array_equal(s.sigma, 7.68 + d * np.ones(90))
+    assert len({(s.seed, s.stream) for s in sims}) == len(sims)  # distinct noise streams
+
+
+def test_script_grid():
+    sims = sweep.homogeneous(1, 0, grid="script")
+    assert sims[21].dG == np.linspace(-0.1, 0.5, 20, endpoint=False)[1]
+    assert sims[21].dsigma == np.linspace(-1, 1, 20, endpoint=False)[1]
+
+
+def test_maps_list():
+    sims = sweep.maps(1, 1, n_iterations=1, n_init=25)
+    ach = np.load(os.path.join(datasets.DATA, "DIST_VAChT_feobv_hc18_aghourian.npy"))
+    na = np.load(os.path.join(datasets.DATA, "DIST_LC_proj.npy"))
+    ach, na = ach / ach.mean(), na / na.mean()  # in the file dtype (float32 for VAChT), :57/:65
+    s = sims[47]
+    np.testing.assert_array_equal(s.G, 0.16 + s.dG * ach)  # whole_sweep_both_maps.py:103-106
+    np.testing.assert_array_equal(s.sigma, 7.68 + s.dsigma * na)
+    assert s.seed == 25
+
+
+def test_many_seeds_list():
+    sims = sweep.many_seeds("map", n_iterations=2)
+    assert [(s.seed, s.state) for s in sims] == list(itertools.product(range(2), datasets.STATES))
+    n1 = sims[1]
+    ach = datasets.load_map(datasets.MAPNAMES_ACH[1])
+    np.testing.assert_allclose(n1.G, 0.16 + ach * 0.18)
+    assert sweep.many_seeds("homo", 1)[3].dG == -0.04
+
+
+def test_shard_is_reference_round_robin():
+    sims = sweep.homogeneous(2)
+    parts = [sweep.shard(sims, r, 7) for r in range(7)]
+    assert sorted(s.index for p in parts for s in p) == list(range(len(sims)))
+    assert all(s.index % 7 == r for r, p in enumerate(parts) for s in p)
+
+
+def _shipped(kind):
+    import pandas as pd
+    return pd.read_csv(os.path.join(GOLD, f"shipped_{kind}_head.csv"))
+
+
+@pytest.mark.parametrize("kind", ["homo", "maps", "shuf"])
+def test_rank_files_collapse_to_shipped_format(tmp_path, kind):
+    """TSV lines written like whole_sweep_both.py:116, collapsed, reproduce the
+    shipped comma-separated table byte for byte."""
+    df = _shipped(kind)
+    paths = {}
+    for rank, g in df.groupby("rank", sort=False):
+        sims = [sweep.Sim(0, int(r.seed), r.delta_G, r.delta_sigma, None, None, 0) for r in g.itertuples()]
+        rows = [{c: getattr(r, c) for c in sweep.METRIC_COLS} for r in g.itertuples()]
+        p = str(tmp_path / f"r{rank}")
+        sweep.append_rows(p, rank, sims, rows)
+        paths[rank] = p
+    out = tmp_path / "collapsed.txt"
+    sweep.collapse([paths[r] for r in dict.fromkeys(df["rank"])], out)
+    with open(os.path.join(GOLD, f"shipped_{kind}_head.csv")) as f:
+        want = f.read()
+    assert out.read_text() == want
+
+
+def test_resume_skips_done(tmp_path):
+    sims = sweep.homogeneous(1)[:5]
+    rows = [{c: 0.5 for c in sweep.METRIC_COLS} for _ in sims]
+    p = str(tmp_path / "rank0")
+    sweep.append_rows(p, 0, sims[:3], rows[:3])
+    have = sweep.done_keys(p)
+    todo = [s for s in sims if (s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") not in have]
+    assert [s.index for s in todo] == [3, 4]
+    sweep.append_rows(p, 0, todo, rows[3:])
+    with open(p) as f:
+        lines = f.readlines()
+    assert lines[0].rstrip("\n").split("\t") == sweep.HEADER and len(lines) == 6
+
+
+def _gather_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sims = sweep.shard(sweep.homogeneous(1)[:11], rank, world)
+    rows = [{c: s.index + 0.01 * j for j, c in enumerate(sweep.METRIC_COLS)} for s in sims]
+    t = sweep.gather_table(sweep.rows_table(rank, sims, rows), dist, torch.device("cpu"))
+    q.put((rank, t))
+    dist.destroy_process_group()
+
+
+def test_gather_gloo_world2():
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        t = got[r]
+        assert t.shape == (11, 20)
+        np.testing.assert_array_equal(t[:, 1], np.arange(11))
+        np.testing.assert_array_equal(t[:, 0], np.arange(11) % 2)
+        np.testing.assert_allclose(t[:, 4], np.arange(11))
+
+
+@pytest.mark.gpu
+def test_sweep_main_short(tmp_path, cuda):
+    """End to end: a short-schedule homogeneous sweep of 6 simulations writes
+    the rank TSV and the collapsed table; a second invocation resumes (no new rows)."""
+    import pandas as pd
+    out = str(tmp_path)
+    sweep.main(["homo", "--seeds", "1", "--short", "--limit", "6", "--out", out, "--tag", "t"])
+    df = pd.read_csv(os.path.join(out, "t.txt"))
+    assert len(df) == 6 and list(df.columns) == sweep.HEADER
+    assert np.isfinite(df[sweep.METRIC_COLS].to_numpy()).all()
+    assert (df["corrW"].abs() <= 1).all() and (df["peakfreq"] > 0).all()
+    sweep.main(["homo", "--seeds", "1", "--short", "--limit", "6", "--out", out, "--tag", "t"])
+    assert len(pd.read_csv(os.path.join(out, "t.txt"))) == 6
