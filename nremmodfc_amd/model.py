@@ -118,7 +118,7 @@ class Batch:
         self.B = B = keys.shape[0]
 
         def per_node(x):
-            x = torch.as_tensor(np.asarray(x, dtype=np.float64))
+            x = torch.from_numpy(np.array(x, dtype=np.float64))
             if x.ndim == 0:
                 x = x.expand(B, N)
             elif x.ndim == 1 and x.shape[0] == B:

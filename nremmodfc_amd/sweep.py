@@ -20,7 +20,9 @@ from __future__ import annotations
 import argparse
 import dataclasses
 import itertools
+import json
 import os
+import time
 import pickle
 from typing import List, Optional
 
@@ -145,6 +147,7 @@ def run_sims(sims: List[Sim], sc, empfcs, schedule=None, precision="f32", batch=
     from .model import sim_keys
     from .pipeline import run_sweep
     rows, fcs = [], []
+    timings = []
     for b0 in range(0, len(sims), batch):
         part = sims[b0:b0 + batch]
         G = np.stack([s.G for s in part])
@@ -153,10 +156,33 @@ def run_sims(sims: List[Sim], sc, empfcs, schedule=None, precision="f32", batch=
         res = run_sweep(sc, G, S, keys, empfcs, schedule, precision=precision, want_fc=want_fc, device=device,
                         progress=progress)
         cols = res.columns()
+        timings.append(dict(res.timings, sims=len(part)))
         rows += [{c: float(cols[c][i]) for c in METRIC_COLS} for i in range(len(part))]
         if want_fc:
             fcs += list(res.fc)
+    run_sims.last_timings = timings
     return rows, (fcs if want_fc else None)
+
+
+class Progress:
+    """Progress lines about once a minute (synchronising the device so the line
+    reflects finished work, not just queued launches)."""
+
+    def __init__(self, rank, every_s=60.0):
+        import time
+        self.t0 = self.last = time.perf_counter()
+        self.rank, self.every = rank, every_s
+
+    def __call__(self, phase, step, total):
+        import time
+        import torch
+        now = time.perf_counter()
+        if now - self.last >= self.every:
+            torch.cuda.synchronize()
+            now = time.perf_counter()
+            print(f"[rank {self.rank}] {phase}: step {step}/{total} ({100 * step / total:.1f}%), "
+                  f"{now - self.t0:.0f} s", flush=True)
+            self.last = now
 
 
 def rows_table(rank, sims, rows):
@@ -256,7 +282,13 @@ def main(argv=None):
         path = os.path.join(args.out, "temp", f"{tag}_rank{rank}")
         have = done_keys(path)
         todo = [s for s in mine if (s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") not in have]
-        rows, _ = run_sims(todo, sc, empfcs, sched, args.precision, args.batch, device)
+        t0 = time.perf_counter()
+        rows, _ = run_sims(todo, sc, empfcs, sched, args.precision, args.batch, device, progress=Progress(rank))
+        wall = time.perf_counter() - t0
+        n_steps = len(todo) * sc.shape[0] * sched.n_total
+        print(json.dumps({"rank": rank, "sims": len(todo), "wall_s": wall, "node_steps": n_steps,
+                          "node_steps_per_s": n_steps / wall if wall else None,
+                          "batches": getattr(run_sims, "last_timings", None)}), flush=True)
         append_rows(path, rank, todo, rows)
         table = rows_table(rank, todo, rows)
         if dist:
