@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define WCSDE_ABI_VERSION 1
+#define WCSDE_ABI_VERSION 2
 
 /* Noise stream (the reference's numba RNG is seeded from os.urandom and never
  * reproducible; the build defines its own): Philox4x32-10 with
@@ -46,7 +46,7 @@ enum wc_precision { WC_F32 = 0, WC_F64 = 1 };
 enum wc_error {
     WC_OK = 0,
     WC_EINVAL = -1,     /* bad shape / argument */
-    WC_EUNSUPPORTED = -2, /* N outside the compiled tile range */
+    WC_EUNSUPPORTED = -2, /* size outside what the kernels support */
     WC_EWORKSPACE = -3, /* workspace NULL or too small */
     WC_EHIP = -4        /* a HIP runtime call failed */
 };
@@ -66,9 +66,12 @@ typedef struct wc_params {
 int wcsde_abi_version(void);
 const char* wc_last_error(void);
 
-/* Bytes of device workspace wc_integrate needs for an N-node connectome (the
- * connectome's MFMA A-operand image, rebuilt by every call). */
-size_t wc_workspace_size(int N, int precision);
+/* Bytes of device workspace wc_integrate needs for B simulations of an N-node
+ * connectome.  N <= 96: the connectome's MFMA A-operand image only (state stays
+ * in registers for the whole call).  N > 96: the A-operand image plus the
+ * tile-major state image and the double-buffered E operand (~48 B per
+ * node-simulation in fp32, padded to multiples of 64 nodes and simulations). */
+size_t wc_workspace_size(int B, int N, int precision);
 
 /*
  * Advance B independent simulations by `nsteps` Euler-Maruyama steps of the
@@ -95,6 +98,9 @@ size_t wc_workspace_size(int N, int precision);
  *            terms of 3-way split operands with fp32 accumulation (fp32-
  *            equivalent); a_ie as a compensated fp32 pair;
  *            WC_F64: everything fp64 (the parity mode).
+ *  N <= 96   one launch integrates all nsteps with the state in registers;
+ *  N > 96    one GEMM-shaped launch per Euler step (wc_sde_large.hip), the
+ *            state in the workspace between steps; same noise stream.
  */
 int wc_integrate(const wc_params* p, int precision, int B, int N,
                  const double* sc, const double* G, const double* sigmaE,

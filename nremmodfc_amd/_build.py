@@ -28,7 +28,8 @@ def _stale(target, deps):
 
 def build(force=False, verbose=False):
     srcs = sources()
-    deps = srcs + [os.path.join(ROOT, "include", "wcsde.h")]
+    deps = srcs + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    deps.append(os.path.join(ROOT, "include", "wcsde.h"))
     if not force and not _stale(LIB, deps):
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

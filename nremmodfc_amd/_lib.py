@@ -41,7 +41,7 @@ c_int, c_i64, c_sz, c_dbl, c_vp = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t,
 _SIGNATURES = {
     "wcsde_abi_version": (c_int, []),
     "wc_last_error": (ctypes.c_char_p, []),
-    "wc_workspace_size": (c_sz, [c_int, c_int]),
+    "wc_workspace_size": (c_sz, [c_int, c_int, c_int]),
     "wc_integrate": (c_int, [ctypes.POINTER(WCParamsC), c_int, c_int, c_int,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_i64, c_i64, c_dbl, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),

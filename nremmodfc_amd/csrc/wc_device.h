@@ -1,0 +1,167 @@
+// wc_device.h -- device helpers shared by the Wilson-Cowan integrators (gfx950):
+// the Philox4x32-10 noise stream of include/wcsde.h, Box-Muller normals,
+// precision traits (sigmoid, MFMA), the 3-way bf16 split and the compensated
+// a_ie accumulator.  Both wc_sde.hip (N <= 96, register-resident) and
+// wc_sde_large.hip (N > 96, one launch per step) draw the SAME normals for a
+// given (key, step, node), so the two paths integrate the same stochastic
+// trajectory.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/wcsde.h"
+
+namespace wcdev {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// ---------------- noise: Philox4x32-10 (must match oracle/wc_oracle.c) ----------------
+// key = (WC_PHILOX_KEY0, WC_PHILOX_KEY1) for every simulation (wave-uniform: the
+// key schedule lives in SGPRs); counter = (step lo32, (step hi16 << 16) | quad,
+// simkey lo32, simkey hi32).  Outputs feed two Box-Muller pairs -> the standard
+// normals of nodes 4*quad + 0..3.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
+}
+
+__device__ __forceinline__ void mul_wide(uint32_t a, uint32_t m, uint32_t& hi, uint32_t& lo) {
+    uint64_t r;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "s"(m) : "vcc");  // one op for hi:lo
+    hi = (uint32_t)(r >> 32);
+    lo = (uint32_t)r;
+}
+
+__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
+    uint32_t k0 = WC_PHILOX_KEY0, k1 = WC_PHILOX_KEY1;
+    // round 1: c0 (the step) is wave-uniform -> scalar multiply
+    {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        c0 = xor3(hi1, c1, k0);
+        c1 = lo1;
+        c2 = xor3(hi0, c3, k1);
+        c3 = lo0;
+    }
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+        uint32_t hi0, lo0, hi1, lo1;
+        mul_wide(c0, 0xD2511F53u, hi0, lo0);
+        mul_wide(c2, 0xCD9E8D57u, hi1, lo1);
+        c0 = xor3(hi1, c1, k0);
+        c1 = lo1;
+        c2 = xor3(hi0, c3, k1);
+        c3 = lo0;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__device__ __forceinline__ void philox_ctr(uint64_t step, uint32_t quad, uint64_t simkey, uint32_t out[4]) {
+    philox((uint32_t)step, ((uint32_t)(step >> 32) << 16) | quad, (uint32_t)simkey, (uint32_t)(simkey >> 32),
+           out);
+}
+
+// u = (2*(x>>9)+1) * 2^-24, exact in fp32 and fp64, in (0,1)
+__device__ __forceinline__ float u01f(uint32_t x) { return (float)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8f; }
+__device__ __forceinline__ double u01d(uint32_t x) { return (double)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8; }
+
+// fp32: hardware transcendentals.  ln u = log2(u) ln2; v_sin/v_cos take
+// revolutions (sin(2 pi x)).  Inputs are never denormal: u >= 2^-24.
+__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, float z[4]) {
+    uint32_t x[4];
+    philox_ctr(step, q, key, x);
+    const float r0 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[0])));
+    const float r1 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[2])));
+    const float a0 = u01f(x[1]), a1 = u01f(x[3]);
+    z[0] = r0 * __builtin_amdgcn_cosf(a0);
+    z[1] = r0 * __builtin_amdgcn_sinf(a0);
+    z[2] = r1 * __builtin_amdgcn_cosf(a1);
+    z[3] = r1 * __builtin_amdgcn_sinf(a1);
+}
+
+// fp64: correctly rounded-ish libm (ocml); sincospi reduces 2u exactly
+__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, double z[4]) {
+    uint32_t x[4];
+    philox_ctr(step, q, key, x);
+    const double r0 = sqrt(-2.0 * log(u01d(x[0])));
+    const double r1 = sqrt(-2.0 * log(u01d(x[2])));
+    double s0, c0, s1, c1;
+    sincospi(2.0 * u01d(x[1]), &s0, &c0);
+    sincospi(2.0 * u01d(x[3]), &s1, &c1);
+    z[0] = r0 * c0;
+    z[1] = r0 * s0;
+    z[2] = r1 * c1;
+    z[3] = r1 * s1;
+}
+
+// ---------------- precision traits ----------------
+template <typename Real> struct Tr;
+template <> struct Tr<float> {
+    typedef f32x4 acc_t;
+    __device__ static __forceinline__ acc_t mfma(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // logistic 1/(1+exp(-(x-mu)*sigma)) with sl = sigma*log2(e) precomputed
+    __device__ static __forceinline__ float sig(float x, float mu, float sl) {
+        return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((mu - x) * sl));
+    }
+    __device__ static __forceinline__ float slope(double s) { return (float)(s * 1.4426950408889634); }
+    // C/D row of a 16x16x4 f32 tile is (lane>>4)*4 + reg: identity row->node map
+    __host__ __device__ static __forceinline__ int row_node(int rho) { return rho; }
+};
+template <> struct Tr<double> {
+    typedef f64x4 acc_t;
+    __device__ static __forceinline__ acc_t mfma(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    __device__ static __forceinline__ double sig(double x, double mu, double s) {
+        return 1.0 / (1.0 + exp(-(x - mu) * s));
+    }
+    __device__ static __forceinline__ double slope(double s) { return s; }
+    // f64 16x16x4 C/D row is (lane>>4) + 4*reg; permute so that lane group g,
+    // register r still means node 4g + r of the tile
+    __host__ __device__ static __forceinline__ int row_node(int rho) { return 4 * (rho & 3) + (rho >> 2); }
+};
+
+// v = hi + mid + lo, each a bf16: |v - hi - mid - lo| <= 2^-27 |v|
+__device__ __forceinline__ void split3(const float v[4], bf16x4& hi, bf16x4& mid, bf16x4& lo) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const __bf16 h = (__bf16)v[i];
+        const float r = v[i] - (float)h;
+        const __bf16 m = (__bf16)r;
+        hi[i] = h;
+        mid[i] = m;
+        lo[i] = (__bf16)(r - (float)m);
+    }
+}
+
+// Plasticity variable a_ie: fp64, or a compensated fp32 pair (increments of
+// ~1e-6 on a ~2.5 are below fp32 half-ulp: plain fp32 would drop them).
+template <bool kPair> struct AccA;
+template <> struct AccA<false> {
+    double v;
+    __device__ void set(double x) { v = x; }
+    __device__ double get() const { return v; }
+    template <typename Real> __device__ Real val() const { return (Real)v; }
+    __device__ void add(float inc) { v += (double)inc; }
+    __device__ void add(double inc) { v += inc; }
+};
+template <> struct AccA<true> {
+    float hi, lo;
+    __device__ void set(double x) { hi = (float)x; lo = (float)(x - (double)hi); }
+    __device__ double get() const { return (double)hi + (double)lo; }
+    template <typename Real> __device__ Real val() const { return (Real)(hi + lo); }
+    __device__ void add(float inc) {  // Kahan-Babuska: |hi| >> |inc|
+        const float t = inc + lo;
+        const float s = hi + t;
+        lo = t - (s - hi);
+        hi = s;
+    }
+};
+
+
+}  // namespace wcdev

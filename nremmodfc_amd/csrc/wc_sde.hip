@@ -27,126 +27,21 @@
 #include <stdio.h>
 #include <string.h>
 #include "wc_common.h"
+#include "wc_device.h"
+
+// N > 96: wc_sde_large.hip (one GEMM-shaped launch per Euler step)
+size_t wc_large_workspace_size(int B, int N, int precision);
+int wc_large_integrate(const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
+                       const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
+                       int64_t nsteps, double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI,
+                       void* recA, void* workspace, hipStream_t st);
 
 namespace {
+using namespace wcdev;
 
 
 constexpr int kSims = 16;     // simulations per workgroup (MFMA N dimension)
 constexpr int kMaxTiles = 6;  // N <= 96 on the register-resident path
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef double f64x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-
-// ---------------- noise: Philox4x32-10 (must match oracle/wc_oracle.c) ----------------
-// key = (WC_PHILOX_KEY0, WC_PHILOX_KEY1) for every simulation (wave-uniform: the
-// key schedule lives in SGPRs); counter = (step lo32, (step hi16 << 16) | quad,
-// simkey lo32, simkey hi32).  Outputs feed two Box-Muller pairs -> the standard
-// normals of nodes 4*quad + 0..3.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
-}
-
-__device__ __forceinline__ void mul_wide(uint32_t a, uint32_t m, uint32_t& hi, uint32_t& lo) {
-    uint64_t r;
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "s"(m) : "vcc");  // one op for hi:lo
-    hi = (uint32_t)(r >> 32);
-    lo = (uint32_t)r;
-}
-
-__device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t out[4]) {
-    uint32_t k0 = WC_PHILOX_KEY0, k1 = WC_PHILOX_KEY1;
-    // round 1: c0 (the step) is wave-uniform -> scalar multiply
-    {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        c0 = xor3(hi1, c1, k0);
-        c1 = lo1;
-        c2 = xor3(hi0, c3, k1);
-        c3 = lo0;
-    }
-#pragma unroll
-    for (int r = 1; r < 10; ++r) {
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-        uint32_t hi0, lo0, hi1, lo1;
-        mul_wide(c0, 0xD2511F53u, hi0, lo0);
-        mul_wide(c2, 0xCD9E8D57u, hi1, lo1);
-        c0 = xor3(hi1, c1, k0);
-        c1 = lo1;
-        c2 = xor3(hi0, c3, k1);
-        c3 = lo0;
-    }
-    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
-}
-
-__device__ __forceinline__ void philox_ctr(uint64_t step, uint32_t quad, uint64_t simkey, uint32_t out[4]) {
-    philox((uint32_t)step, ((uint32_t)(step >> 32) << 16) | quad, (uint32_t)simkey, (uint32_t)(simkey >> 32),
-           out);
-}
-
-// u = (2*(x>>9)+1) * 2^-24, exact in fp32 and fp64, in (0,1)
-__device__ __forceinline__ float u01f(uint32_t x) { return (float)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8f; }
-__device__ __forceinline__ double u01d(uint32_t x) { return (double)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8; }
-
-// fp32: hardware transcendentals.  ln u = log2(u) ln2; v_sin/v_cos take
-// revolutions (sin(2 pi x)).  Inputs are never denormal: u >= 2^-24.
-__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, float z[4]) {
-    uint32_t x[4];
-    philox_ctr(step, q, key, x);
-    const float r0 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[0])));
-    const float r1 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[2])));
-    const float a0 = u01f(x[1]), a1 = u01f(x[3]);
-    z[0] = r0 * __builtin_amdgcn_cosf(a0);
-    z[1] = r0 * __builtin_amdgcn_sinf(a0);
-    z[2] = r1 * __builtin_amdgcn_cosf(a1);
-    z[3] = r1 * __builtin_amdgcn_sinf(a1);
-}
-
-// fp64: correctly rounded-ish libm (ocml); sincospi reduces 2u exactly
-__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, double z[4]) {
-    uint32_t x[4];
-    philox_ctr(step, q, key, x);
-    const double r0 = sqrt(-2.0 * log(u01d(x[0])));
-    const double r1 = sqrt(-2.0 * log(u01d(x[2])));
-    double s0, c0, s1, c1;
-    sincospi(2.0 * u01d(x[1]), &s0, &c0);
-    sincospi(2.0 * u01d(x[3]), &s1, &c1);
-    z[0] = r0 * c0;
-    z[1] = r0 * s0;
-    z[2] = r1 * c1;
-    z[3] = r1 * s1;
-}
-
-// ---------------- precision traits ----------------
-template <typename Real> struct Tr;
-template <> struct Tr<float> {
-    typedef f32x4 acc_t;
-    __device__ static __forceinline__ acc_t mfma(float a, float b, acc_t c) {
-        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-    }
-    // logistic 1/(1+exp(-(x-mu)*sigma)) with sl = sigma*log2(e) precomputed
-    __device__ static __forceinline__ float sig(float x, float mu, float sl) {
-        return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((mu - x) * sl));
-    }
-    __device__ static __forceinline__ float slope(double s) { return (float)(s * 1.4426950408889634); }
-    // C/D row of a 16x16x4 f32 tile is (lane>>4)*4 + reg: identity row->node map
-    __host__ __device__ static __forceinline__ int row_node(int rho) { return rho; }
-};
-template <> struct Tr<double> {
-    typedef f64x4 acc_t;
-    __device__ static __forceinline__ acc_t mfma(double a, double b, acc_t c) {
-        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-    }
-    __device__ static __forceinline__ double sig(double x, double mu, double s) {
-        return 1.0 / (1.0 + exp(-(x - mu) * s));
-    }
-    __device__ static __forceinline__ double slope(double s) { return s; }
-    // f64 16x16x4 C/D row is (lane>>4) + 4*reg; permute so that lane group g,
-    // register r still means node 4g + r of the tile
-    __host__ __device__ static __forceinline__ int row_node(int rho) { return 4 * (rho & 3) + (rho >> 2); }
-};
 
 struct KArgs {
     double a_ee, a_ei, a_ii, tauE, tauI, P, rhoE, rE, rI, mu, sigmaI, sqdtD, dtSim;
@@ -211,19 +106,6 @@ __global__ void build_frag_bf16(const double* __restrict__ sc, int N, bf16x8* __
     for (int p = 0; p < 3; ++p) frag[(size_t)(tc * 3 + p) * 64 + lane] = part[p];
 }
 
-// v = hi + mid + lo, each a bf16: |v - hi - mid - lo| <= 2^-27 |v|
-__device__ __forceinline__ void split3(const float v[4], bf16x4& hi, bf16x4& mid, bf16x4& lo) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const __bf16 h = (__bf16)v[i];
-        const float r = v[i] - (float)h;
-        const __bf16 m = (__bf16)r;
-        hi[i] = h;
-        mid[i] = m;
-        lo[i] = (__bf16)(r - (float)m);
-    }
-}
-
 // ---------------- variants ----------------
 enum : int {
     V_FRAG_REGS = 1,  // A-operand fragments held in registers (else streamed from LDS each step)
@@ -232,30 +114,6 @@ enum : int {
     V_KAHAN_A = 8,    // fp32: a_ie as a compensated fp32 pair instead of fp64
     V_BF16X6 = 32,    // fp32 coupling as the six bf16 cross terms (product)
     V_BF16X3 = 64,    // ablation: only the three leading terms (~2^-17 relative)
-};
-
-// Plasticity variable a_ie: fp64, or a compensated fp32 pair (increments of
-// ~1e-6 on a ~2.5 are below fp32 half-ulp: plain fp32 would drop them).
-template <bool kPair> struct AccA;
-template <> struct AccA<false> {
-    double v;
-    __device__ void set(double x) { v = x; }
-    __device__ double get() const { return v; }
-    template <typename Real> __device__ Real val() const { return (Real)v; }
-    __device__ void add(float inc) { v += (double)inc; }
-    __device__ void add(double inc) { v += inc; }
-};
-template <> struct AccA<true> {
-    float hi, lo;
-    __device__ void set(double x) { hi = (float)x; lo = (float)(x - (double)hi); }
-    __device__ double get() const { return (double)hi + (double)lo; }
-    template <typename Real> __device__ Real val() const { return (Real)(hi + lo); }
-    __device__ void add(float inc) {  // Kahan-Babuska: |hi| >> |inc|
-        const float t = inc + lo;
-        const float s = hi + t;
-        lo = t - (s - hi);
-        hi = s;
-    }
 };
 
 template <typename Real, int NT, int NW, int VAR, int MINW>
@@ -659,9 +517,9 @@ int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const 
         return wc_set_err(WC_EINVAL, "wc_integrate: NULL array argument");
     if (precision != WC_F32 && precision != WC_F64) return wc_set_err(WC_EINVAL, "wc_integrate: bad precision");
     if (rec_every > 0 && !recE) return wc_set_err(WC_EINVAL, "wc_integrate: rec_every > 0 needs recE");
-    if (tiles_for(N) > kMaxTiles) return wc_set_err(WC_EUNSUPPORTED, "wc_integrate: N > 96 not supported");
-    if (!workspace || ws_bytes < frag_bytes(N, precision))
-        return wc_set_err(WC_EWORKSPACE, "wc_integrate: workspace too small");
+    if (N > 4 * 65535) return wc_set_err(WC_EUNSUPPORTED, "wc_integrate: N > 262140 (Philox quad is 16 bits)");
+    const size_t need = tiles_for(N) > kMaxTiles ? wc_large_workspace_size(B, N, precision) : frag_bytes(N, precision);
+    if (!workspace || ws_bytes < need) return wc_set_err(WC_EWORKSPACE, "wc_integrate: workspace too small");
     ka.a_ee = p->a_ee; ka.a_ei = p->a_ei; ka.a_ii = p->a_ii;
     ka.tauE = p->tauE; ka.tauI = p->tauI; ka.P = p->P; ka.rhoE = p->rhoE;
     ka.rE = p->rE; ka.rI = p->rI; ka.mu = p->mu; ka.sigmaI = p->sigmaI;
@@ -680,8 +538,9 @@ int wcsde_abi_version(void) { return WCSDE_ABI_VERSION; }
 
 const char* wc_last_error(void) { return wc_errbuf(); }
 
-size_t wc_workspace_size(int N, int precision) {
-    if (N <= 0) return 0;
+size_t wc_workspace_size(int B, int N, int precision) {
+    if (N <= 0 || B <= 0) return 0;
+    if (tiles_for(N) > kMaxTiles) return wc_large_workspace_size(B, N, precision);
     // the diagnostic f32-MFMA variants need the native image; size for the larger
     const int nt = tiles_for(N);
     const size_t native = (size_t)nt * nt * 64 * 4 * (precision == WC_F64 ? 8 : 4);
@@ -698,6 +557,9 @@ int wc_integrate(const wc_params* p, int precision, int B, int N, const double* 
                        recE, recI, recA, workspace, ws_bytes);
     if (rc != WC_OK || nsteps == 0) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (tiles_for(N) > kMaxTiles)
+        return wc_large_integrate(p, precision, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every,
+                                  rec_ld, recE, recI, recA, workspace, st);
     return precision == WC_F64 ? launch_f64(ka, sc, workspace, st) : launch_f32(ka, sc, workspace, st);
 }
 
@@ -710,7 +572,7 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
                        recE, nullptr, nullptr, workspace, ws_bytes);
     if (rc != WC_OK || nsteps == 0) return rc;
     if (tiles_for(N) != 6) return wc_set_err(WC_EUNSUPPORTED, "wc_diag_integrate: needs 81 <= N <= 96");
-    if (ws_bytes < wc_workspace_size(N, WC_F32)) return wc_set_err(WC_EWORKSPACE, "wc_diag_integrate: workspace");
+    if (ws_bytes < wc_workspace_size(B, N, WC_F32)) return wc_set_err(WC_EWORKSPACE, "wc_diag_integrate: workspace");
     return launch_diag(variant, ka, sc, workspace, static_cast<hipStream_t>(stream));
 }
 

@@ -1,0 +1,438 @@
+// wc_sde_large.hip -- Wilson-Cowan Euler-Maruyama integrator for N > 96 (gfx950).
+//
+// Same model and noise stream as wc_sde.hip (wilsonCowan wc:77-83, run
+// wc:86-137) for connectomes too large to keep in registers (BASELINE config 5:
+// N = 1000).  The dense coupling of one Euler step over the whole batch is a
+// GEMM, D[node][sim] = CM . E (M = N, N = B, K = N), so each Euler step is one
+// launch of a GEMM-shaped kernel whose epilogue is the elementwise update:
+//
+//   * workgroup tile = 64 nodes x 64 simulations, 4 waves of 32 x 32
+//     (2 x 2 MFMA 16x16 tiles); K loop over 32-node chunks;
+//   * fp32 product path: CM and E as three bf16 parts each, six cross terms on
+//     v_mfma_f32_16x16x32_bf16 (fp32-equivalent, as in wc_sde.hip); the split
+//     E of the next step is written by the epilogue straight into the
+//     B-operand fragment layout, so the GEMM reads 16 B per lane, 1 KB per
+//     wave instruction, no LDS and no shuffles;
+//   * fp64 parity path: v_mfma_f64_16x16x4_f64 on fp64 E;
+//   * the MFMA D fragment of a lane is 4 consecutive nodes of one simulation
+//     = exactly one Philox4x32-10 call (quad = node/4): the epilogue draws the
+//     noise, integrates E, I, a_ie (Kahan pair in fp32) and records;
+//   * I, a_ie, G and sigmaE stay in a tile-major workspace image laid out like
+//     the D fragment (one 16-B load per lane per array); the launch boundary
+//     is the grid-wide barrier between steps (~1.5 us, cheaper than any
+//     software grid barrier on this part: MI355X guide, "boundary").
+// wc_integrate converts the caller's fp64 [B][N] state into this image at
+// entry and back at exit.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "wc_common.h"
+#include "wc_device.h"
+
+namespace {
+using namespace wcdev;
+
+constexpr int kTile = 64;  // node and simulation padding unit (workgroup tile edge)
+
+struct Geo {
+    int B, N, Bp, Np, MT, NC, KC4;  // MT = Np/16 node tiles; NC = Np/32 bf16 chunks; KC4 = Np/4 f64 chunks
+    size_t o_frag, o_E, o_I, o_Ahi, o_Alo, o_G, o_S, o_X0, o_X1, total;
+};
+
+size_t al(size_t x) { return (x + 255) & ~size_t(255); }
+
+Geo geometry(int B, int N, int precision) {
+    Geo g{};
+    g.B = B;
+    g.N = N;
+    g.Bp = (B + kTile - 1) / kTile * kTile;
+    g.Np = (N + kTile - 1) / kTile * kTile;
+    g.MT = g.Np / 16;
+    g.NC = g.Np / 32;
+    g.KC4 = g.Np / 4;
+    const size_t cells = (size_t)g.Bp * g.Np;
+    size_t o = 0;
+    g.o_frag = o;
+    if (precision == WC_F32) {
+        o += al((size_t)g.MT * g.NC * 3 * 64 * 16);
+        g.o_E = o; o += al(cells * 4);
+        g.o_I = o; o += al(cells * 4);
+        g.o_Ahi = o; o += al(cells * 4);
+        g.o_Alo = o; o += al(cells * 4);
+        g.o_G = o; o += al(cells * 4);
+        g.o_S = o; o += al(cells * 4);
+        g.o_X0 = o; o += al(cells * 6);  // 3 bf16 parts
+        g.o_X1 = o; o += al(cells * 6);
+    } else {
+        o += al((size_t)g.MT * g.KC4 * 64 * 8);
+        g.o_E = 0;
+        g.o_I = o; o += al(cells * 8);
+        g.o_Ahi = o; o += al(cells * 8);
+        g.o_Alo = 0;
+        g.o_G = o; o += al(cells * 8);
+        g.o_S = o; o += al(cells * 8);
+        g.o_X0 = o; o += al(cells * 8);
+        g.o_X1 = o; o += al(cells * 8);
+    }
+    g.total = o;
+    return g;
+}
+
+struct LArgs {
+    double a_ee, a_ei, a_ii, tauE, tauI, P, rhoE, rE, rI, mu, sigmaI, sqdtD, dtSim, tau_ip;
+    const uint64_t* keys;
+    void* recE;
+    void* recI;
+    void* recA;
+    int64_t rec_ld;
+    int64_t step0;
+    char* ws;
+    Geo g;
+};
+
+// tile-major index of (sim b, node n): [b/16][n/16][lane = 16*((n%16)/4) + b%16][n%4]
+__host__ __device__ __forceinline__ size_t tm_index(const Geo& g, int b, int n) {
+    const int lane = 16 * ((n & 15) >> 2) + (b & 15);
+    return ((((size_t)(b >> 4) * g.MT + (n >> 4)) * 64 + lane) << 2) + (n & 3);
+}
+
+// bf16 B-operand image of the split E: element (part p, node n, sim b) at
+// [p][c = n/32][b][g = (n%16)/4][h = (n/16)%2][r = n%4]  (8 bf16 = one lane's operand)
+__host__ __device__ __forceinline__ size_t xb_index(const Geo& g, int p, int b, int n) {
+    const int c = n >> 5, h = (n >> 4) & 1, gg = (n & 15) >> 2, r = n & 3;
+    return ((((size_t)p * g.NC + c) * g.Bp + b) * 4 + gg) * 8 + 4 * h + r;
+}
+
+// f64 B operand: E of node n = 4c + k, sim b at [c][b][k]
+__host__ __device__ __forceinline__ size_t x64_index(const Geo& g, int b, int n) {
+    return ((size_t)(n >> 2) * g.Bp + b) * 4 + (n & 3);
+}
+
+// ---- A-operand images of CM ----
+__global__ void frag_bf16_kernel(const double* __restrict__ sc, Geo g, bf16x8* __restrict__ frag) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // ((m*NC + c)*64 + lane)
+    if (idx >= g.MT * g.NC * 64) return;
+    const int lane = idx & 63;
+    const int mc = idx >> 6;
+    const int m = mc / g.NC, c = mc % g.NC;
+    const int row = 16 * m + (lane & 15);
+    bf16x8 part[3];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        const int col = 16 * (2 * c + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);
+        const double x = (row < g.N && col < g.N) ? sc[(size_t)row * g.N + col] : 0.0;
+        const __bf16 h = (__bf16)(float)x;
+        const double r1 = x - (double)(float)h;
+        const __bf16 mm = (__bf16)(float)r1;
+        part[0][jj] = h;
+        part[1][jj] = mm;
+        part[2][jj] = (__bf16)(float)(r1 - (double)(float)mm);
+    }
+#pragma unroll
+    for (int p = 0; p < 3; ++p) frag[((size_t)mc * 3 + p) * 64 + lane] = part[p];
+}
+
+__global__ void frag_f64_kernel(const double* __restrict__ sc, Geo g, double* __restrict__ frag) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // ((m*KC4 + c)*64 + lane)
+    if (idx >= g.MT * g.KC4 * 64) return;
+    const int lane = idx & 63;
+    const int mc = idx >> 6;
+    const int m = mc / g.KC4, c = mc % g.KC4;
+    const int row = 16 * m + Tr<double>::row_node(lane & 15);
+    const int col = 4 * c + (lane >> 4);
+    frag[idx] = (row < g.N && col < g.N) ? sc[(size_t)row * g.N + col] : 0.0;
+}
+
+// ---- state in/out ----
+template <typename Real>
+__global__ void prep_kernel(LArgs a, const double* __restrict__ G, const double* __restrict__ sigmaE,
+                            const double* __restrict__ E, const double* __restrict__ I, const double* __restrict__ A) {
+    const Geo& g = a.g;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)g.Bp * g.Np) return;
+    const int b = (int)(idx / g.Np), n = (int)(idx % g.Np);
+    const bool ok = b < g.B && n < g.N;
+    const size_t o = ok ? (size_t)b * g.N + n : 0;
+    const double e = ok ? E[o] : 0.0, in = ok ? I[o] : 0.0, ai = ok ? A[o] : 0.0;
+    const double gc = ok ? G[o] : 0.0, s = ok ? sigmaE[o] : 0.0;
+    const size_t t = tm_index(g, b, n);
+    if constexpr (sizeof(Real) == 4) {
+        reinterpret_cast<float*>(a.ws + g.o_E)[t] = (float)e;
+        reinterpret_cast<float*>(a.ws + g.o_I)[t] = (float)in;
+        AccA<true> acc;
+        acc.set(ai);
+        reinterpret_cast<float*>(a.ws + g.o_Ahi)[t] = acc.hi;
+        reinterpret_cast<float*>(a.ws + g.o_Alo)[t] = acc.lo;
+        reinterpret_cast<float*>(a.ws + g.o_G)[t] = (float)gc;
+        reinterpret_cast<float*>(a.ws + g.o_S)[t] = Tr<float>::slope(s);
+        float v[4] = {(float)e, 0.f, 0.f, 0.f};
+        bf16x4 h, m, l;
+        split3(v, h, m, l);
+        __bf16* X = reinterpret_cast<__bf16*>(a.ws + g.o_X0);
+        X[xb_index(g, 0, b, n)] = h[0];
+        X[xb_index(g, 1, b, n)] = m[0];
+        X[xb_index(g, 2, b, n)] = l[0];
+    } else {
+        reinterpret_cast<double*>(a.ws + g.o_I)[t] = in;
+        reinterpret_cast<double*>(a.ws + g.o_Ahi)[t] = ai;
+        reinterpret_cast<double*>(a.ws + g.o_G)[t] = gc;
+        reinterpret_cast<double*>(a.ws + g.o_S)[t] = s;
+        reinterpret_cast<double*>(a.ws + g.o_X0)[x64_index(g, b, n)] = e;
+    }
+}
+
+template <typename Real>
+__global__ void finish_kernel(LArgs a, int buf, double* __restrict__ E, double* __restrict__ I,
+                              double* __restrict__ A) {
+    const Geo& g = a.g;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)g.B * g.N) return;
+    const int b = (int)(idx / g.N), n = (int)(idx % g.N);
+    const size_t t = tm_index(g, b, n);
+    if constexpr (sizeof(Real) == 4) {
+        E[idx] = reinterpret_cast<const float*>(a.ws + g.o_E)[t];
+        I[idx] = reinterpret_cast<const float*>(a.ws + g.o_I)[t];
+        A[idx] = (double)reinterpret_cast<const float*>(a.ws + g.o_Ahi)[t] +
+                 (double)reinterpret_cast<const float*>(a.ws + g.o_Alo)[t];
+    } else {
+        E[idx] = reinterpret_cast<const double*>(a.ws + (buf ? g.o_X1 : g.o_X0))[x64_index(g, b, n)];
+        I[idx] = reinterpret_cast<const double*>(a.ws + g.o_I)[t];
+        A[idx] = reinterpret_cast<const double*>(a.ws + g.o_Ahi)[t];
+    }
+}
+
+// blockIdx -> (sim block, node block); consecutive workgroups land on different
+// XCDs (round robin), so give each XCD a contiguous range of sim blocks: the
+// 16 node blocks that share one sim block's B operand then share an L2.
+__device__ __forceinline__ void tile_of(const Geo& g, int& sb, int& mb) {
+    const int MB = g.Np / kTile;
+    const int W = (g.Bp / kTile) * MB;
+    int wid = blockIdx.x;
+    if ((W & 7) == 0) wid = (blockIdx.x & 7) * (W >> 3) + (blockIdx.x >> 3);
+    sb = wid / MB;
+    mb = wid % MB;
+}
+
+// one Euler step of every simulation; rec_row >= 0: record the state before the update
+template <typename Real>
+__global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec_row, int buf) {
+    typedef typename Tr<Real>::acc_t acc_t;
+    typedef __attribute__((ext_vector_type(4))) Real real4;
+    const Geo& g = a.g;
+    int sb, mb;
+    tile_of(g, sb, mb);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int j = lane & 15, gq = lane >> 4;
+    const int m0 = mb * 4 + (w & 1) * 2;   // this wave's node tiles m0, m0+1
+    const int s0 = sb * 4 + (w >> 1) * 2;  // and sim tiles s0, s0+1
+
+    acc_t acc[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) acc[u][v] = acc_t{0, 0, 0, 0};
+
+    if constexpr (sizeof(Real) == 4) {
+        const bf16x8* F = reinterpret_cast<const bf16x8*>(a.ws + g.o_frag);
+        const bf16x8* X = reinterpret_cast<const bf16x8*>(a.ws + (buf ? g.o_X1 : g.o_X0));
+        const size_t pstride = (size_t)g.NC * g.Bp * 4;  // bf16x8 units per part
+#pragma unroll 2
+        for (int c = 0; c < g.NC; ++c) {
+            bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) fa[u][p] = F[(((size_t)(m0 + u) * g.NC + c) * 3 + p) * 64 + lane];
+#pragma unroll
+            for (int v = 0; v < 2; ++v)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    fb[v][p] = X[p * pstride + ((size_t)c * g.Bp + 16 * (s0 + v) + j) * 4 + gq];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    // small terms first (2^-18, 2^-9, 1), as in wc_sde.hip
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][2], fb[v][0], acc[u][v], 0, 0, 0);
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[v][1], acc[u][v], 0, 0, 0);
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][2], acc[u][v], 0, 0, 0);
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[v][0], acc[u][v], 0, 0, 0);
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][1], acc[u][v], 0, 0, 0);
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][0], acc[u][v], 0, 0, 0);
+                }
+        }
+    } else {
+        const double* F = reinterpret_cast<const double*>(a.ws + g.o_frag);
+        const double* X = reinterpret_cast<const double*>(a.ws + (buf ? g.o_X1 : g.o_X0));
+#pragma unroll 4
+        for (int c = 0; c < g.KC4; ++c) {
+            double fa[2], fb[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) fa[u] = F[((size_t)(m0 + u) * g.KC4 + c) * 64 + lane];
+#pragma unroll
+            for (int v = 0; v < 2; ++v) fb[v] = X[((size_t)c * g.Bp + 16 * (s0 + v) + j) * 4 + gq];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) acc[u][v] = Tr<double>::mfma(fa[u], fb[v], acc[u][v]);
+        }
+    }
+
+    // ---- epilogue: the elementwise update of wc:77-83 on the D fragments ----
+    const Real a_ee = (Real)a.a_ee, a_ei = (Real)a.a_ei, a_ii = (Real)a.a_ii;
+    const Real P = (Real)a.P, rhoE = (Real)a.rhoE, rE = (Real)a.rE, rI = (Real)a.rI;
+    const Real mu = (Real)a.mu, slI = Tr<Real>::slope(a.sigmaI), sqdtD = (Real)a.sqdtD;
+    const Real dtE = (Real)(a.dtSim / a.tauE), dtI = (Real)(a.dtSim / a.tauI), dtA = (Real)(a.dtSim / a.tau_ip);
+    const Real dt = (Real)a.dtSim, tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;
+    const uint64_t gstep = (uint64_t)(a.step0 + s);
+    const size_t BN = (size_t)g.B * g.N;
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        const int b = 16 * (s0 + v) + j;
+        const bool live = b < g.B;
+        const uint64_t key = a.keys[live ? b : g.B - 1];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int mt = m0 + u;
+            const int n0 = 16 * mt + 4 * gq;
+            const size_t t4 = ((size_t)(s0 + v) * g.MT + mt) * 64 + lane;  // real4 index of the tile-major image
+            real4* Iw = reinterpret_cast<real4*>(a.ws + g.o_I);
+            real4* Ahw = reinterpret_cast<real4*>(a.ws + g.o_Ahi);
+            const real4 Gv = reinterpret_cast<const real4*>(a.ws + g.o_G)[t4];
+            const real4 Sv = reinterpret_cast<const real4*>(a.ws + g.o_S)[t4];
+            real4 Ev, Iv = Iw[t4];
+            AccA<sizeof(Real) == 4> Av[4];
+            real4* Xn;  // next step's E image (f64) / tile-major E (f32)
+            if constexpr (sizeof(Real) == 4) {
+                real4* Ew = reinterpret_cast<real4*>(a.ws + g.o_E);
+                Ev = Ew[t4];
+                Xn = Ew;
+                const real4 hi = Ahw[t4], lo = reinterpret_cast<const real4*>(a.ws + g.o_Alo)[t4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    Av[r].hi = hi[r];
+                    Av[r].lo = lo[r];
+                }
+            } else {
+                const real4* Xc = reinterpret_cast<const real4*>(a.ws + (buf ? g.o_X1 : g.o_X0));
+                const size_t x4 = (size_t)(4 * mt + gq) * g.Bp + b;  // [c][b][4] as real4
+                Ev = Xc[x4];
+                Xn = reinterpret_cast<real4*>(a.ws + (buf ? g.o_X0 : g.o_X1));
+                const real4 av = Ahw[t4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Av[r].set(av[r]);
+            }
+            if (rec_row >= 0 && live) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = n0 + r;
+                    if (n < g.N) {
+                        const size_t cc = (size_t)b * g.N + n;
+                        const size_t o = a.rec_ld ? cc * a.rec_ld + rec_row : (size_t)rec_row * BN + cc;
+                        static_cast<Real*>(a.recE)[o] = Ev[r];
+                        if (a.recI) static_cast<Real*>(a.recI)[o] = Iv[r];
+                        if (a.recA) static_cast<Real*>(a.recA)[o] = (Real)Av[r].get();
+                    }
+                }
+            }
+            Real z[4];
+            quad_normals(gstep, (uint32_t)(4 * mt + gq), key, z);
+            real4 En, In;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const Real e = Ev[r], in = Iv[r];
+                const Real ai = Av[r].template val<Real>();
+                const Real xE = a_ee * e - ai * in + Gv[r] * acc[u][v][r] + P + sqdtD * z[r];
+                const Real SE = Tr<Real>::sig(xE, mu, Sv[r]);
+                const Real SI = Tr<Real>::sig(a_ei * e - a_ii * in, mu, slI);
+                const bool pad = n0 + r >= g.N;  // padding nodes stay exactly 0 (zero B-operand rows)
+                if constexpr (sizeof(Real) == 8) {
+                    En[r] = pad ? 0.0 : e + dt * ((-e + (1 - rE * e) * SE) / tauE);
+                    In[r] = in + dt * ((-in + (1 - rI * in) * SI) / tauI);
+                    Av[r].add(dt * ((in * (e - rhoE)) / tau_ip));
+                } else {
+                    En[r] = pad ? 0.f : e + dtE * (-e + (1 - rE * e) * SE);
+                    In[r] = in + dtI * (-in + (1 - rI * in) * SI);
+                    Av[r].add(dtA * (in * (e - rhoE)));
+                }
+            }
+            Iw[t4] = In;
+            if constexpr (sizeof(Real) == 4) {
+                Xn[t4] = En;
+                real4 hi, lo;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    hi[r] = Av[r].hi;
+                    lo[r] = Av[r].lo;
+                }
+                Ahw[t4] = hi;
+                reinterpret_cast<real4*>(a.ws + g.o_Alo)[t4] = lo;
+                // split E into the next step's B-operand image (8 B per part per lane)
+                float ev[4] = {En[0], En[1], En[2], En[3]};
+                bf16x4 ph[3];
+                split3(ev, ph[0], ph[1], ph[2]);
+                bf16x4* Xo = reinterpret_cast<bf16x4*>(a.ws + (buf ? g.o_X0 : g.o_X1));
+#pragma unroll
+                for (int p = 0; p < 3; ++p) Xo[xb_index(g, p, b, n0) >> 2] = ph[p];
+            } else {
+                Xn[(size_t)(4 * mt + gq) * g.Bp + b] = En;
+                real4 av;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) av[r] = Av[r].get();
+                Ahw[t4] = av;
+            }
+        }
+    }
+}
+
+template <typename Real>
+int run_large(const wc_params* p, int B, int N, const double* sc, const double* G, const double* sigmaE,
+              const uint64_t* keys, double* E, double* I, double* A, int64_t step0, int64_t nsteps, double tau_ip,
+              int64_t rec_every, int64_t rec_ld, void* recE, void* recI, void* recA, void* workspace,
+              hipStream_t st) {
+    LArgs a{};
+    a.a_ee = p->a_ee; a.a_ei = p->a_ei; a.a_ii = p->a_ii; a.tauE = p->tauE; a.tauI = p->tauI;
+    a.P = p->P; a.rhoE = p->rhoE; a.rE = p->rE; a.rI = p->rI; a.mu = p->mu; a.sigmaI = p->sigmaI;
+    a.sqdtD = p->sqdtD; a.dtSim = p->dtSim; a.tau_ip = tau_ip;
+    a.keys = keys; a.recE = recE; a.recI = recI; a.recA = recA; a.rec_ld = rec_ld; a.step0 = step0;
+    a.ws = static_cast<char*>(workspace);
+    a.g = geometry(B, N, sizeof(Real) == 4 ? WC_F32 : WC_F64);
+    const Geo& g = a.g;
+    if constexpr (sizeof(Real) == 4) {
+        const int n = g.MT * g.NC * 64;
+        hipLaunchKernelGGL(frag_bf16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc, g,
+                           reinterpret_cast<bf16x8*>(a.ws + g.o_frag));
+    } else {
+        const int n = g.MT * g.KC4 * 64;
+        hipLaunchKernelGGL(frag_f64_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc, g,
+                           reinterpret_cast<double*>(a.ws + g.o_frag));
+    }
+    const size_t cells = (size_t)g.Bp * g.Np;
+    hipLaunchKernelGGL(prep_kernel<Real>, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, a, G, sigmaE, E,
+                       I, A);
+    const int W = (g.Bp / kTile) * (g.Np / kTile);
+    for (int64_t s = 0; s < nsteps; ++s) {
+        const int rec_row = (rec_every > 0 && s % rec_every == 0) ? (int)(s / rec_every) : -1;
+        hipLaunchKernelGGL(step_kernel<Real>, dim3(W), dim3(256), 0, st, a, (int)s, rec_row, (int)(s & 1));
+    }
+    const size_t bn = (size_t)B * N;
+    hipLaunchKernelGGL(finish_kernel<Real>, dim3((unsigned)((bn + 255) / 256)), dim3(256), 0, st, a,
+                       (int)(nsteps & 1), E, I, A);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
+}
+
+}  // namespace
+
+// internal entry points used by wc_sde.hip's dispatcher
+size_t wc_large_workspace_size(int B, int N, int precision) { return geometry(B, N, precision).total; }
+
+int wc_large_integrate(const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
+                       const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
+                       int64_t nsteps, double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI,
+                       void* recA, void* workspace, hipStream_t st) {
+    if (precision == WC_F64)
+        return run_large<double>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld,
+                                 recE, recI, recA, workspace, st);
+    return run_large<float>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld, recE,
+                            recI, recA, workspace, st);
+}

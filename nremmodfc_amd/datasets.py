@@ -32,3 +32,21 @@ def load_map(name, n=90):
     the reference does, and only then is widened to float64."""
     m = np.ones(n) if name == "HOMO" else np.load(os.path.join(DATA, name + ".npy"))
     return (m / m.mean()).astype(np.float64)
+
+
+def synthetic_sc(n=1000, seed=1000, density=0.395, mean_rowsum=2.51):
+    """Synthetic connectome for the N=1000 configuration: symmetric,
+    uniform weights on a random support of the given density, zero diagonal,
+    scaled so the mean row sum matches SC_opti_25julio (2.51)."""
+    rng = np.random.default_rng(seed)
+    w = rng.uniform(size=(n, n))
+    mask = rng.uniform(size=(n, n)) < density
+    m = np.triu(w * mask, 1)
+    m = m + m.T
+    return m * (mean_rowsum / m.sum(axis=1).mean())
+
+
+def synthetic_map(n=1000, seed=1001):
+    """Seeded log-normal heterogeneity map with mean 1 (N=1000 maps mode)."""
+    m = np.random.default_rng(seed).lognormal(0.0, 0.3, n)
+    return m / m.mean()

@@ -137,7 +137,7 @@ class Batch:
         self.E = torch.full((B, N), p.E0, dtype=torch.float64, device=self.device)
         self.I = torch.full((B, N), p.I0, dtype=torch.float64, device=self.device)
         self.A = torch.full((B, N), p.a_ie_0, dtype=torch.float64, device=self.device)
-        nbytes = _lib.lib().wc_workspace_size(N, _PREC[precision])
+        nbytes = _lib.lib().wc_workspace_size(B, N, _PREC[precision])
         self.ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=self.device)
         self.step = 0  # global step counter (Philox counter of the next step)
         self._pc = p.to_c()

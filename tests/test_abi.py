@@ -30,10 +30,15 @@ def test_library_exports_header_symbols():
 def test_abi_version_and_workspace():
     from nremmodfc_amd import _lib
     L = _lib.lib()
-    assert L.wcsde_abi_version() == 1
-    assert L.wc_workspace_size(90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16   # bf16x6 image
-    assert L.wc_workspace_size(90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
-    assert L.wc_workspace_size(16, _lib.WC_F32) == 2 * 1 * 3 * 64 * 16
+    assert L.wcsde_abi_version() == 2
+    assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16   # bf16x6 image
+    assert L.wc_workspace_size(20000, 90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
+    assert L.wc_workspace_size(1, 16, _lib.WC_F32) == 2 * 1 * 3 * 64 * 16
+    # N > 96 (wc_sde_large.hip): bf16x3 A image + 6 fp32 state arrays + 2 x 3 bf16 E images, padded to 64
+    Bp, Np = 2560, 1024
+    want = (Np // 16) * (Np // 32) * 3 * 64 * 16 + Bp * Np * (6 * 4 + 2 * 6)
+    assert L.wc_workspace_size(2500, 1000, _lib.WC_F32) == want
+    assert L.wc_workspace_size(2500, 1000, _lib.WC_F64) == (Np // 16) * (Np // 4) * 64 * 8 + Bp * Np * 6 * 8
 
 
 def test_invalid_arguments_fail_loudly():
@@ -45,9 +50,12 @@ def test_invalid_arguments_fail_loudly():
                         None, 0, None)
     assert rc == -1
     assert b"invalid" in L.wc_last_error()
-    rc = L.wc_integrate(ctypes.byref(p), 0, 4, 200, *([ctypes.c_void_p(16)] * 7), 0, 1, 1.0, 0, 0,
+    rc = L.wc_integrate(ctypes.byref(p), 0, 4, 300_000, *([ctypes.c_void_p(16)] * 7), 0, 1, 1.0, 0, 0,
                         None, None, None, ctypes.c_void_p(16), 1 << 20, None)
     assert rc == -2
+    rc = L.wc_integrate(ctypes.byref(p), 0, 2500, 1000, *([ctypes.c_void_p(16)] * 7), 0, 1, 1.0, 0, 0,
+                        None, None, None, ctypes.c_void_p(16), 1 << 20, None)
+    assert rc == -3  # the N > 96 path needs its state image
     # the signal-chain entry points validate before touching the device too
     cfg = _lib.WCBoldCfgC()
     cfg.dec, cfg.neq, cfg.n_total = 1000, 2000, 2010  # fewer than neq + 16 samples

@@ -1,0 +1,85 @@
+"""N > 96 integrator (wc_sde_large.hip: one GEMM-shaped launch per Euler step)
+vs the CPU oracle, same Philox stream as the N <= 96 path.
+
+Tolerances as tests/test_sde_gpu.py: fp64 max |dE| <= 1e-9; fp32 (bf16x6
+coupling, fp32 state, compensated a_ie) max 2e-3 / rms 2e-4 over short horizons.
+Sizes cover BASELINE config 5 (N = 1000 synthetic connectome) and ragged tails
+(B and N not multiples of the 64 x 64 workgroup tile).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from nremmodfc_amd import datasets
+from nremmodfc_amd.model import Batch, driver_params, sim_keys
+from tests.test_sde_gpu import run_pair, tol
+
+pytestmark = pytest.mark.gpu
+
+
+def _sc(N, seed):
+    return datasets.synthetic_sc(N, seed=seed)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("N,B", [(97, 3), (200, 70), (1000, 5)])
+def test_large_vs_oracle(cuda, prec, N, B):
+    sc = _sc(N, N)
+    rng = np.random.default_rng(B)
+    G = 0.16 + rng.uniform(-0.1, 0.3, B)
+    S = 7.68 + rng.uniform(-0.2, 0.2, B)
+    keys = sim_keys(list(range(B)), [N] * B)
+    n = 200 if N < 1000 else 120
+    g, o, gb, ob, _ = run_pair(sc, G, S, keys, n // 2, n // 2, n, 7, prec)
+    mx, rms = tol(prec)
+    d = np.abs(g - o)
+    assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
+    for x, y in ((gb.E, ob.E), (gb.I, ob.I), (gb.A, ob.A)):
+        assert np.abs(x.cpu().numpy() - y).max() <= mx
+
+
+def test_large_maps_mode(cuda):
+    """Per-node G and sigmaE (maps mode) at N = 1000."""
+    N, B = 1000, 4
+    sc = _sc(N, 7)
+    m = datasets.synthetic_map(N)
+    G = np.stack([0.16 + d * m for d in (-0.1, 0.0, 0.1, 0.28)])
+    S = np.stack([7.68 + d * m for d in (0.18, -0.2, 0.0, 0.1)])
+    keys = sim_keys([9] * B, list(range(B)))
+    g, o, *_ = run_pair(sc, G, S, keys, 40, 40, 80, 20, "f64")
+    assert np.abs(g - o).max() <= 1e-9
+
+
+def test_large_chunking_and_ring_layout(cuda):
+    """Chunked calls equal one call (fp64 bit-exact); node-major ring records
+    (rec_ld > 0, the sweep pipeline's layout) equal the time-major ones."""
+    N, B = 130, 3
+    sc = _sc(N, 3)
+    keys = sim_keys([1, 2, 3], [0, 0, 0])
+    a = Batch(sc, 0.16, 7.68, keys, precision="f64")
+    rec = torch.empty((10, B, N), dtype=torch.float64, device="cuda")
+    a.integrate(100, 2.0, 10, rec)
+    b = Batch(sc, 0.16, 7.68, keys, precision="f64")
+    ld = 16
+    ring = torch.zeros(B * N * ld, dtype=torch.float64, device="cuda")
+    b.integrate(50, 2.0, 10, ring, rec_ld=ld)
+    b.integrate(50, 2.0, 10, ring[5:], rec_ld=ld)
+    torch.cuda.synchronize()
+    assert torch.equal(a.E, b.E) and torch.equal(a.I, b.I) and torch.equal(a.A, b.A)
+    nm = ring.view(B, N, ld)[:, :, :10].permute(2, 0, 1)
+    assert torch.equal(nm, rec)
+
+
+def test_large_f32_tracks_f64_statistics(cuda):
+    N, B = 1000, 8
+    sc = _sc(N, 11)
+    keys = sim_keys(list(range(B)), [0] * B)
+    out = {}
+    for prec in ("f32", "f64"):
+        b = Batch(sc, 0.16, 7.68, keys, precision=prec)
+        b.integrate(2000, 0.05)
+        rec = torch.empty((200, B, N), dtype=b.rec_dtype, device="cuda")
+        b.integrate(4000, 2.0, 20, rec)
+        out[prec] = rec.double().mean(0).cpu().numpy()
+    assert np.abs(out["f32"] - out["f64"]).max() < 0.02
