@@ -35,6 +35,9 @@ int wc_large_integrate(const wc_params* p, int precision, int B, int N, const do
                        const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
                        int64_t nsteps, double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI,
                        void* recA, void* workspace, hipStream_t st);
+int wc_large_diag(int variant, const wc_params* p, int B, int N, const double* sc, const double* G,
+                  const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
+                  int64_t nsteps, double tau_ip, void* workspace, hipStream_t st);
 
 namespace {
 using namespace wcdev;
@@ -571,6 +574,11 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
     int rc = make_args(ka, p, WC_F32, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, 0,
                        recE, nullptr, nullptr, workspace, ws_bytes);
     if (rc != WC_OK || nsteps == 0) return rc;
+    if (variant >= 100) {
+        if (tiles_for(N) <= kMaxTiles) return wc_set_err(WC_EUNSUPPORTED, "wc_diag_integrate: variants >= 100 need N > 96");
+        return wc_large_diag(variant, p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, workspace,
+                             static_cast<hipStream_t>(stream));
+    }
     if (tiles_for(N) != 6) return wc_set_err(WC_EUNSUPPORTED, "wc_diag_integrate: needs 81 <= N <= 96");
     if (ws_bytes < wc_workspace_size(B, N, WC_F32)) return wc_set_err(WC_EWORKSPACE, "wc_diag_integrate: workspace");
     return launch_diag(variant, ka, sc, workspace, static_cast<hipStream_t>(stream));

@@ -9,10 +9,12 @@
 //   * workgroup tile = 64 nodes x 64 simulations, 4 waves of 32 x 32
 //     (2 x 2 MFMA 16x16 tiles); K loop over 32-node chunks;
 //   * fp32 product path: CM and E as three bf16 parts each, six cross terms on
-//     v_mfma_f32_16x16x32_bf16 (fp32-equivalent, as in wc_sde.hip); the split
-//     E of the next step is written by the epilogue straight into the
-//     B-operand fragment layout, so the GEMM reads 16 B per lane, 1 KB per
-//     wave instruction, no LDS and no shuffles;
+//     v_mfma_f32_16x16x32_bf16 (fp32-equivalent, as in wc_sde.hip).  CM's
+//     parts are pre-split in the A-operand image; E is kept as ONE fp32 image
+//     in B-operand order (the epilogue writes it in place) and split exactly
+//     (hi + mid + lo == v for any fp32 v) while a chunk is staged into LDS:
+//     each workgroup fetches every A/E chunk once into a double-buffered LDS
+//     stage and its waves read their fragments with ds_read_b128;
 //   * fp64 parity path: v_mfma_f64_16x16x4_f64 on fp64 E;
 //   * the MFMA D fragment of a lane is 4 consecutive nodes of one simulation
 //     = exactly one Philox4x32-10 call (quad = node/4): the epilogue draws the
@@ -54,14 +56,14 @@ Geo geometry(int B, int N, int precision) {
     g.o_frag = o;
     if (precision == WC_F32) {
         o += al((size_t)g.MT * g.NC * 3 * 64 * 16);
-        g.o_E = o; o += al(cells * 4);
+        g.o_E = 0;  // E lives in the fp32 operand image X (exact: no separate copy)
         g.o_I = o; o += al(cells * 4);
         g.o_Ahi = o; o += al(cells * 4);
         g.o_Alo = o; o += al(cells * 4);
         g.o_G = o; o += al(cells * 4);
         g.o_S = o; o += al(cells * 4);
-        g.o_X0 = o; o += al(cells * 6);  // 3 bf16 parts
-        g.o_X1 = o; o += al(cells * 6);
+        g.o_X0 = o; o += al(cells * 4);  // fp32 E, split to bf16 parts while staged into LDS
+        g.o_X1 = o; o += al(cells * 4);
     } else {
         o += al((size_t)g.MT * g.KC4 * 64 * 8);
         g.o_E = 0;
@@ -95,11 +97,12 @@ __host__ __device__ __forceinline__ size_t tm_index(const Geo& g, int b, int n) 
     return ((((size_t)(b >> 4) * g.MT + (n >> 4)) * 64 + lane) << 2) + (n & 3);
 }
 
-// bf16 B-operand image of the split E: element (part p, node n, sim b) at
-// [p][c = n/32][b][g = (n%16)/4][h = (n/16)%2][r = n%4]  (8 bf16 = one lane's operand)
-__host__ __device__ __forceinline__ size_t xb_index(const Geo& g, int p, int b, int n) {
+// fp32 B-operand image of E: node n, sim b at [c = n/32][b][g = (n%16)/4][h = (n/16)%2][r = n%4]:
+// the 8 floats of (c, b, g) are, in order, lane (g, b%16)'s B operand of k-chunk c
+// (matches the A image: k element jj = 4h + r <-> node 16(2c + h) + 4g + r)
+__host__ __device__ __forceinline__ size_t x32_index(const Geo& g, int b, int n) {
     const int c = n >> 5, h = (n >> 4) & 1, gg = (n & 15) >> 2, r = n & 3;
-    return ((((size_t)p * g.NC + c) * g.Bp + b) * 4 + gg) * 8 + 4 * h + r;
+    return (((size_t)c * g.Bp + b) * 4 + gg) * 8 + 4 * h + r;
 }
 
 // f64 B operand: E of node n = 4c + k, sim b at [c][b][k]
@@ -156,7 +159,7 @@ __global__ void prep_kernel(LArgs a, const double* __restrict__ G, const double*
     const double gc = ok ? G[o] : 0.0, s = ok ? sigmaE[o] : 0.0;
     const size_t t = tm_index(g, b, n);
     if constexpr (sizeof(Real) == 4) {
-        reinterpret_cast<float*>(a.ws + g.o_E)[t] = (float)e;
+        reinterpret_cast<float*>(a.ws + g.o_X0)[x32_index(g, b, n)] = (float)e;
         reinterpret_cast<float*>(a.ws + g.o_I)[t] = (float)in;
         AccA<true> acc;
         acc.set(ai);
@@ -164,13 +167,6 @@ __global__ void prep_kernel(LArgs a, const double* __restrict__ G, const double*
         reinterpret_cast<float*>(a.ws + g.o_Alo)[t] = acc.lo;
         reinterpret_cast<float*>(a.ws + g.o_G)[t] = (float)gc;
         reinterpret_cast<float*>(a.ws + g.o_S)[t] = Tr<float>::slope(s);
-        float v[4] = {(float)e, 0.f, 0.f, 0.f};
-        bf16x4 h, m, l;
-        split3(v, h, m, l);
-        __bf16* X = reinterpret_cast<__bf16*>(a.ws + g.o_X0);
-        X[xb_index(g, 0, b, n)] = h[0];
-        X[xb_index(g, 1, b, n)] = m[0];
-        X[xb_index(g, 2, b, n)] = l[0];
     } else {
         reinterpret_cast<double*>(a.ws + g.o_I)[t] = in;
         reinterpret_cast<double*>(a.ws + g.o_Ahi)[t] = ai;
@@ -189,7 +185,7 @@ __global__ void finish_kernel(LArgs a, int buf, double* __restrict__ E, double* 
     const int b = (int)(idx / g.N), n = (int)(idx % g.N);
     const size_t t = tm_index(g, b, n);
     if constexpr (sizeof(Real) == 4) {
-        E[idx] = reinterpret_cast<const float*>(a.ws + g.o_E)[t];
+        E[idx] = reinterpret_cast<const float*>(a.ws + (buf ? g.o_X1 : g.o_X0))[x32_index(g, b, n)];
         I[idx] = reinterpret_cast<const float*>(a.ws + g.o_I)[t];
         A[idx] = (double)reinterpret_cast<const float*>(a.ws + g.o_Ahi)[t] +
                  (double)reinterpret_cast<const float*>(a.ws + g.o_Alo)[t];
@@ -200,12 +196,15 @@ __global__ void finish_kernel(LArgs a, int buf, double* __restrict__ E, double* 
     }
 }
 
-// blockIdx -> (sim block, node block); consecutive workgroups land on different
-// XCDs (round robin), so give each XCD a contiguous range of sim blocks: the
-// 16 node blocks that share one sim block's B operand then share an L2.
+// blockIdx -> (sim block, node block).  Consecutive workgroups land on
+// different XCDs (round robin); each XCD gets a contiguous range of SIM blocks
+// with all their node blocks.  Every XCD then streams the whole connectome image
+// once per step (6.3 MB at N = 1000, shared by its concurrently running
+// workgroups through its L2) and only its own columns of E -- less fabric
+// traffic than splitting nodes, which would make every XCD read all of E.
 __device__ __forceinline__ void tile_of(const Geo& g, int& sb, int& mb) {
-    const int MB = g.Np / kTile;
-    const int W = (g.Bp / kTile) * MB;
+    const int MB = g.Np / kTile, SB = g.Bp / kTile;
+    const int W = SB * MB;
     int wid = blockIdx.x;
     if ((W & 7) == 0) wid = (blockIdx.x & 7) * (W >> 3) + (blockIdx.x >> 3);
     sb = wid / MB;
@@ -213,7 +212,9 @@ __device__ __forceinline__ void tile_of(const Geo& g, int& sb, int& mb) {
 }
 
 // one Euler step of every simulation; rec_row >= 0: record the state before the update
-template <typename Real>
+// DIAG (ablation, tools/diag_large.py): 1 = no chunk fetch (LDS reused),
+// 2 = no MFMA, 3 = no epilogue state traffic (noise + math only), 0 = product
+template <typename Real, int DIAG = 0>
 __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec_row, int buf) {
     typedef typename Tr<Real>::acc_t acc_t;
     typedef __attribute__((ext_vector_type(4))) Real real4;
@@ -222,35 +223,80 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
     tile_of(g, sb, mb);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int j = lane & 15, gq = lane >> 4;
-    const int m0 = mb * 4 + (w & 1) * 2;   // this wave's node tiles m0, m0+1
-    const int s0 = sb * 4 + (w >> 1) * 2;  // and sim tiles s0, s0+1
+    // wave w computes node tiles m0, m0+1 x sim tiles s0, s0+1 of the 64 x 64 workgroup tile
+    constexpr int NU = 2, NV = 2;
+    const int m0 = mb * 4 + (w & 1) * 2;
+    const int s0 = sb * 4 + (w >> 1) * 2;
 
-    acc_t acc[2][2];
+    acc_t acc[NU][NV];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < NU; ++u)
 #pragma unroll
-        for (int v = 0; v < 2; ++v) acc[u][v] = acc_t{0, 0, 0, 0};
+        for (int v = 0; v < NV; ++v) acc[u][v] = acc_t{0, 0, 0, 0};
 
     if constexpr (sizeof(Real) == 4) {
+        // Each 32-node k-chunk of the workgroup's A rows (4 tiles x 3 parts) and
+        // E columns (4 sim tiles x 3 parts) is fetched ONCE per workgroup into a
+        // double-buffered LDS stage (2 x 24 KB; 6 x 16 B per thread, 1-3 KB
+        // contiguous runs), then every wave reads its fragments with
+        // ds_read_b128.  The fetch of chunk c+1 is in flight during chunk c's 96 MFMAs.
+        __shared__ bf16x8 lds[2][2][4 * 3 * 64];  // [stage][A|B][tile*3 + part][lane]
         const bf16x8* F = reinterpret_cast<const bf16x8*>(a.ws + g.o_frag);
-        const bf16x8* X = reinterpret_cast<const bf16x8*>(a.ws + (buf ? g.o_X1 : g.o_X0));
-        const size_t pstride = (size_t)g.NC * g.Bp * 4;  // bf16x8 units per part
-#pragma unroll 2
-        for (int c = 0; c < g.NC; ++c) {
+        const f32x4* X = reinterpret_cast<const f32x4*>(a.ws + (buf ? g.o_X1 : g.o_X0));
+        const int t = threadIdx.x;
+        // A: unit q = t + 256 i (i = 0..2) of the 768-unit pre-split slab: tile = q / 192, rem = q % 192
+        const bf16x8* fsrc[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int q = t + 256 * i;
+            fsrc[i] = F + (size_t)(mb * 4 + q / 192) * g.NC * 192 + q % 192;
+        }
+        // B: thread t = 4 * sim + g loads the 8 fp32 E of (chunk, sim, g) and splits them
+        const int bsim = t >> 2, bg = t & 3;
+        const f32x4* xsrc = X + ((size_t)(sb * 64 + bsim) * 4 + bg) * 2;
+        const int bdst = ((bsim >> 4) * 3) * 64 + 16 * bg + (bsim & 15);  // [tile][part 0][lane]
+        const size_t xstep = (size_t)g.Bp * 4 * 2;
+        // register ring of two in-flight chunks: chunk c+2 is fetched while chunk c
+        // is on the MFMA and chunk c+1 (fetched one iteration earlier) is being stashed
+        bf16x8 ra[2][3];
+        f32x4 rb[2][2];
+        auto fetch = [&](int c, int q) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) ra[q][i] = fsrc[i][(size_t)c * 192];
+            rb[q][0] = xsrc[(size_t)c * xstep];
+            rb[q][1] = xsrc[(size_t)c * xstep + 1];
+        };
+        auto stash = [&](int st, int q) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) lds[st][0][t + 256 * i] = ra[q][i];
+            bf16x4 h0, m0, l0, h1, m1, l1;
+            const float v0[4] = {rb[q][0][0], rb[q][0][1], rb[q][0][2], rb[q][0][3]};
+            const float v1[4] = {rb[q][1][0], rb[q][1][1], rb[q][1][2], rb[q][1][3]};
+            split3(v0, h0, m0, l0);
+            split3(v1, h1, m1, l1);
+            lds[st][1][bdst] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+            lds[st][1][bdst + 64] = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+            lds[st][1][bdst + 128] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+        };
+        const int ua = (w & 1) * 2, ub = (w >> 1) * 2;  // this wave's tiles within the workgroup slab
+        auto body = [&](int c, int q) {  // q = c & 1 (compile-time at each call site)
+            if (DIAG != 1 && c + 2 < g.NC) fetch(c + 2, q);
             bf16x8 fa[2][3], fb[2][3];
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int p = 0; p < 3; ++p) fa[u][p] = F[(((size_t)(m0 + u) * g.NC + c) * 3 + p) * 64 + lane];
-#pragma unroll
-            for (int v = 0; v < 2; ++v)
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    fb[v][p] = X[p * pstride + ((size_t)c * g.Bp + 16 * (s0 + v) + j) * 4 + gq];
+                for (int p = 0; p < 3; ++p) {
+                    fa[u][p] = lds[q][0][((ua + u) * 3 + p) * 64 + lane];
+                    fb[u][p] = lds[q][1][((ub + u) * 3 + p) * 64 + lane];
+                }
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int v = 0; v < 2; ++v) {
+                    if (DIAG == 2) {
+                        acc[u][v][0] += (float)fa[u][0][0] * (float)fb[v][0][0];
+                        continue;
+                    }
                     // small terms first (2^-18, 2^-9, 1), as in wc_sde.hip
                     acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][2], fb[v][0], acc[u][v], 0, 0, 0);
                     acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[v][1], acc[u][v], 0, 0, 0);
@@ -259,21 +305,32 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
                     acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][1], acc[u][v], 0, 0, 0);
                     acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][0], acc[u][v], 0, 0, 0);
                 }
+            // stage q^1 was last read in chunk c-1, before the barrier
+            if (DIAG != 1 && c + 1 < g.NC) stash(q ^ 1, q ^ 1);
+            __syncthreads();
+        };
+        fetch(0, 0);
+        if (g.NC > 1) fetch(1, 1);
+        stash(0, 0);
+        __syncthreads();
+        for (int c = 0; c < g.NC; c += 2) {  // NC is even (Np is a multiple of 64)
+            body(c, 0);
+            body(c + 1, 1);
         }
     } else {
         const double* F = reinterpret_cast<const double*>(a.ws + g.o_frag);
         const double* X = reinterpret_cast<const double*>(a.ws + (buf ? g.o_X1 : g.o_X0));
 #pragma unroll 4
         for (int c = 0; c < g.KC4; ++c) {
-            double fa[2], fb[2];
+            double fa[NU], fb[NV];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) fa[u] = F[((size_t)(m0 + u) * g.KC4 + c) * 64 + lane];
+            for (int u = 0; u < NU; ++u) fa[u] = F[((size_t)(m0 + u) * g.KC4 + c) * 64 + lane];
 #pragma unroll
-            for (int v = 0; v < 2; ++v) fb[v] = X[((size_t)c * g.Bp + 16 * (s0 + v) + j) * 4 + gq];
+            for (int v = 0; v < NV; ++v) fb[v] = X[((size_t)c * g.Bp + 16 * (s0 + v) + j) * 4 + gq];
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < NU; ++u)
 #pragma unroll
-                for (int v = 0; v < 2; ++v) acc[u][v] = Tr<double>::mfma(fa[u], fb[v], acc[u][v]);
+                for (int v = 0; v < NV; ++v) acc[u][v] = Tr<double>::mfma(fa[u], fb[v], acc[u][v]);
         }
     }
 
@@ -286,27 +343,29 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
     const uint64_t gstep = (uint64_t)(a.step0 + s);
     const size_t BN = (size_t)g.B * g.N;
 #pragma unroll
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < NV; ++v) {
         const int b = 16 * (s0 + v) + j;
         const bool live = b < g.B;
         const uint64_t key = a.keys[live ? b : g.B - 1];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < NU; ++u) {
             const int mt = m0 + u;
             const int n0 = 16 * mt + 4 * gq;
             const size_t t4 = ((size_t)(s0 + v) * g.MT + mt) * 64 + lane;  // real4 index of the tile-major image
             real4* Iw = reinterpret_cast<real4*>(a.ws + g.o_I);
             real4* Ahw = reinterpret_cast<real4*>(a.ws + g.o_Ahi);
-            const real4 Gv = reinterpret_cast<const real4*>(a.ws + g.o_G)[t4];
-            const real4 Sv = reinterpret_cast<const real4*>(a.ws + g.o_S)[t4];
-            real4 Ev, Iv = Iw[t4];
+            constexpr bool kState = DIAG != 3;
+            const real4 Gv = kState ? reinterpret_cast<const real4*>(a.ws + g.o_G)[t4] : real4{0.16, 0.16, 0.16, 0.16};
+            const real4 Sv = kState ? reinterpret_cast<const real4*>(a.ws + g.o_S)[t4] : real4{11, 11, 11, 11};
+            real4 Ev, Iv = kState ? Iw[t4] : real4{0.1, 0.1, 0.1, 0.1};
             AccA<sizeof(Real) == 4> Av[4];
             real4* Xn;  // next step's E image (f64) / tile-major E (f32)
             if constexpr (sizeof(Real) == 4) {
-                real4* Ew = reinterpret_cast<real4*>(a.ws + g.o_E);
-                Ev = Ew[t4];
-                Xn = Ew;
-                const real4 hi = Ahw[t4], lo = reinterpret_cast<const real4*>(a.ws + g.o_Alo)[t4];
+                const size_t x4 = x32_index(g, b, n0) >> 2;  // this lane's 4 nodes, one real4
+                Ev = reinterpret_cast<const real4*>(a.ws + (buf ? g.o_X1 : g.o_X0))[x4];
+                Xn = reinterpret_cast<real4*>(a.ws + (buf ? g.o_X0 : g.o_X1)) + x4;
+                const real4 hi = kState ? Ahw[t4] : real4{2.5, 2.5, 2.5, 2.5};
+                const real4 lo = kState ? reinterpret_cast<const real4*>(a.ws + g.o_Alo)[t4] : real4{0, 0, 0, 0};
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     Av[r].hi = hi[r];
@@ -355,9 +414,10 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
                     Av[r].add(dtA * (in * (e - rhoE)));
                 }
             }
-            Iw[t4] = In;
+            if (kState) Iw[t4] = In;
             if constexpr (sizeof(Real) == 4) {
-                Xn[t4] = En;
+                *Xn = En;
+                if (!kState) continue;
                 real4 hi, lo;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -366,13 +426,6 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
                 }
                 Ahw[t4] = hi;
                 reinterpret_cast<real4*>(a.ws + g.o_Alo)[t4] = lo;
-                // split E into the next step's B-operand image (8 B per part per lane)
-                float ev[4] = {En[0], En[1], En[2], En[3]};
-                bf16x4 ph[3];
-                split3(ev, ph[0], ph[1], ph[2]);
-                bf16x4* Xo = reinterpret_cast<bf16x4*>(a.ws + (buf ? g.o_X0 : g.o_X1));
-#pragma unroll
-                for (int p = 0; p < 3; ++p) Xo[xb_index(g, p, b, n0) >> 2] = ph[p];
             } else {
                 Xn[(size_t)(4 * mt + gq) * g.Bp + b] = En;
                 real4 av;
@@ -384,7 +437,7 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
     }
 }
 
-template <typename Real>
+template <typename Real, int DIAG = 0>
 int run_large(const wc_params* p, int B, int N, const double* sc, const double* G, const double* sigmaE,
               const uint64_t* keys, double* E, double* I, double* A, int64_t step0, int64_t nsteps, double tau_ip,
               int64_t rec_every, int64_t rec_ld, void* recE, void* recI, void* recA, void* workspace,
@@ -412,7 +465,7 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
     const int W = (g.Bp / kTile) * (g.Np / kTile);
     for (int64_t s = 0; s < nsteps; ++s) {
         const int rec_row = (rec_every > 0 && s % rec_every == 0) ? (int)(s / rec_every) : -1;
-        hipLaunchKernelGGL(step_kernel<Real>, dim3(W), dim3(256), 0, st, a, (int)s, rec_row, (int)(s & 1));
+        hipLaunchKernelGGL((step_kernel<Real, DIAG>), dim3(W), dim3(256), 0, st, a, (int)s, rec_row, (int)(s & 1));
     }
     const size_t bn = (size_t)B * N;
     hipLaunchKernelGGL(finish_kernel<Real>, dim3((unsigned)((bn + 255) / 256)), dim3(256), 0, st, a,
@@ -435,4 +488,21 @@ int wc_large_integrate(const wc_params* p, int precision, int B, int N, const do
                                  recE, recI, recA, workspace, st);
     return run_large<float>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld, recE,
                             recI, recA, workspace, st);
+}
+
+// ablation variants of the fp32 step kernel (wc_diag_integrate variants 100..103)
+int wc_large_diag(int variant, const wc_params* p, int B, int N, const double* sc, const double* G,
+                  const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
+                  int64_t nsteps, double tau_ip, void* workspace, hipStream_t st) {
+    switch (variant) {
+        case 100: return run_large<float, 0>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, 0, 0,
+                                             nullptr, nullptr, nullptr, workspace, st);
+        case 101: return run_large<float, 1>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, 0, 0,
+                                             nullptr, nullptr, nullptr, workspace, st);
+        case 102: return run_large<float, 2>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, 0, 0,
+                                             nullptr, nullptr, nullptr, workspace, st);
+        case 103: return run_large<float, 3>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, 0, 0,
+                                             nullptr, nullptr, nullptr, workspace, st);
+        default: return wc_set_err(WC_EINVAL, "unknown large-N diagnostic variant");
+    }
 }

@@ -11,7 +11,8 @@ from nremmodfc_amd.model import Batch, sim_keys
 
 def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
-    for B in (2500, 5000, 20000):
+    Bs = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else (2500, 5000, 20000)
+    for B in Bs:
         sc = datasets.synthetic_sc(N)
         rng = np.random.default_rng(0)
         G = 0.16 + rng.uniform(-0.1, 0.3, B)
