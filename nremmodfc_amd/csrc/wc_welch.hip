@@ -38,7 +38,8 @@ template <typename R> __device__ __forceinline__ cx<R> csub(cx<R> a, cx<R> b) { 
 // concurrent FFTs per workgroup: 2 x (ping + pong) x 2000 complex fits 64 KB (fp32) / 128 KB (fp64)
 template <typename R> constexpr int kG = sizeof(R) == 4 ? 4 : 2;
 
-// twiddle table T[m] = exp(-2 pi i m / 4000), m in [0, 4000)
+// twiddle table T[m] = exp(-2 pi i m / 4000), m in [0, 4000): fp64 (tw) and its
+// correctly rounded fp32 copy (tw32, right after the fp64 table)
 __global__ void twiddle_kernel(double* tw) {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= kSeg) return;
@@ -46,6 +47,8 @@ __global__ void twiddle_kernel(double* tw) {
     sincospi(2.0 * m / kSeg, &s, &c);
     tw[2 * m] = c;
     tw[2 * m + 1] = -s;
+    float2* tw32 = reinterpret_cast<float2*>(tw + 2 * kSeg);
+    tw32[m] = make_float2((float)c, (float)-s);
 }
 
 template <typename R>
@@ -220,6 +223,202 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
     }
 }
 
+// ---------------- fp32 product kernel: one wave per column ----------------
+// Each wave owns one column's 2000-point packed FFT in its own 16 KB of LDS and
+// runs it with no workgroup barrier: every radix stage reads all of the wave's
+// butterfly inputs into registers, then writes the outputs in place (the wave
+// owns every point).  Four waves (columns) per workgroup, 64 KB of LDS, two
+// workgroups per CU.  fp32 arithmetic with the correctly rounded fp32 twiddle
+// table; |X_k|^2 summed per lane in fp32 over the wave's ~N/4 columns, then the
+// four waves are combined in fp64 and added to the simulation's fp64 row.
+constexpr int kWv = 4;
+typedef __attribute__((address_space(3))) void* lds_vptr;
+constexpr int kLaneBins = (kBins + 63) / 64;  // 32
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+// in-place radix-RAD Stockham stage (p = product of the previous radices);
+// WIN: stage 1 also detrends and Hann-windows the raw packed samples it reads
+template <int RAD, int P, bool WIN>
+__device__ __forceinline__ void wstage(float2* z, const float2* __restrict__ tw, int lane) {
+    constexpr int S = kFFT / RAD;
+    constexpr int NB = (S + 63) / 64;
+    constexpr int TS = 2 * (kFFT / (P * RAD));  // twiddle index step in the 4000-table
+    float2 u[NB][RAD];
+    float part = 0.f;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+        const int i = lane + 64 * q;
+        if (i < S) {
+#pragma unroll
+            for (int r = 0; r < RAD; ++r) {
+                u[q][r] = z[i + r * S];
+                if constexpr (WIN) part += u[q][r].x + u[q][r].y;
+            }
+        }
+    }
+    if constexpr (WIN) {
+        // the first stage reads every raw sample: column mean (constant detrend), then
+        // the periodic Hann window w(t) = 0.5 - 0.5 cos(2 pi t / 4000) on the packed pairs
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        const float mean = part / (float)kSeg;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            __builtin_amdgcn_sched_barrier(0);  // window-table loads: bounded look-ahead
+            const int i = lane + 64 * q;
+            if (i < S) {
+#pragma unroll
+                for (int r = 0; r < RAD; ++r) {
+                    const int m = i + r * S;  // samples 2m, 2m+1
+                    u[q][r].x = (u[q][r].x - mean) * (0.5f - 0.5f * tw[2 * m].x);
+                    u[q][r].y = (u[q][r].y - mean) * (0.5f - 0.5f * tw[2 * m + 1].x);
+                }
+            }
+        }
+    }
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+        __builtin_amdgcn_sched_barrier(0);  // bound the twiddle-load look-ahead (register pressure)
+        const int i = lane + 64 * q;
+        if (i < S) {
+            const int k = i % P;
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) u[q][r] = cmulf(u[q][r], tw[r * k * TS]);
+            float2 U[RAD];
+            if constexpr (RAD == 4) {
+                const float2 a = make_float2(u[q][0].x + u[q][2].x, u[q][0].y + u[q][2].y);
+                const float2 b = make_float2(u[q][0].x - u[q][2].x, u[q][0].y - u[q][2].y);
+                const float2 c = make_float2(u[q][1].x + u[q][3].x, u[q][1].y + u[q][3].y);
+                const float2 d = make_float2(u[q][1].x - u[q][3].x, u[q][1].y - u[q][3].y);
+                U[0] = make_float2(a.x + c.x, a.y + c.y);
+                U[2] = make_float2(a.x - c.x, a.y - c.y);
+                U[1] = make_float2(b.x + d.y, b.y - d.x);  // b - i d
+                U[3] = make_float2(b.x - d.y, b.y + d.x);  // b + i d
+            } else {
+                const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+                const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+                const float2 t1 = make_float2(u[q][1].x + u[q][4].x, u[q][1].y + u[q][4].y);
+                const float2 t2 = make_float2(u[q][2].x + u[q][3].x, u[q][2].y + u[q][3].y);
+                const float2 t3 = make_float2(u[q][1].x - u[q][4].x, u[q][1].y - u[q][4].y);
+                const float2 t4 = make_float2(u[q][2].x - u[q][3].x, u[q][2].y - u[q][3].y);
+                U[0] = make_float2(u[q][0].x + t1.x + t2.x, u[q][0].y + t1.y + t2.y);
+                const float2 a1 = make_float2(u[q][0].x + c1 * t1.x + c2 * t2.x, u[q][0].y + c1 * t1.y + c2 * t2.y);
+                const float2 a2 = make_float2(u[q][0].x + c2 * t1.x + c1 * t2.x, u[q][0].y + c2 * t1.y + c1 * t2.y);
+                const float2 b1 = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);
+                const float2 b2 = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);
+                U[1] = make_float2(a1.x + b1.y, a1.y - b1.x);
+                U[4] = make_float2(a1.x - b1.y, a1.y + b1.x);
+                U[2] = make_float2(a2.x + b2.y, a2.y - b2.x);
+                U[3] = make_float2(a2.x - b2.y, a2.y + b2.x);
+            }
+            const int j = (i - k) * RAD + k;
+#pragma unroll
+            for (int s2i = 0; s2i < RAD; ++s2i) z[j + s2i * P] = U[s2i];
+        }
+    }
+    wave_sync();
+}
+
+__global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int b = blockIdx.x;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float2* z = reinterpret_cast<float2*>(smem) + w * kFFT;
+    float* zf = reinterpret_cast<float*>(z);
+    const float2* tw = reinterpret_cast<const float2*>(a.tw + 2 * kSeg);
+    const float* E = static_cast<const float*>(a.E);
+    float acc[kLaneBins];
+#pragma unroll
+    for (int i = 0; i < kLaneBins; ++i) acc[i] = 0.f;
+    // ring runs of the segment (<= 5, wave-uniform): sample t of run r is at column offset ro[r] + t
+    int rt[5], ro[5];
+    {
+        int t = 0;
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            rt[r] = t < kSeg ? t : kSeg + 1;
+            ro[r] = 0;
+            if (t < kSeg) {
+                const int64_t ts = a.seg0 + t;
+                const int64_t q = ts / a.slot, rr = ts % a.slot;
+                ro[r] = (int)((q % a.nslots) * a.slot + rr) - t;
+                t += (int)min((int64_t)(kSeg - t), a.slot - rr);
+            }
+        }
+    }
+
+    for (int n = w; n < a.N; n += kWv) {
+        // ---- stage the raw segment into LDS by LDS-DMA: 16 x global_load_lds_dwordx4
+        //      (1 KB per wave instruction); each lane's 16 B lie in one ring run ----
+        const float* col = E + ((int64_t)b * a.N + n) * a.ld;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int t = 256 * i + 4 * lane;
+            if (t < kSeg) {
+                int off = ro[0] + t;
+#pragma unroll
+                for (int r = 1; r < 5; ++r)
+                    if (t >= rt[r]) off = ro[r] + t;
+                __builtin_amdgcn_global_load_lds(col + off, (lds_vptr)(zf + 256 * i), 16, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): the DMA has landed
+        wave_sync();
+        // ---- Stockham 2000 = 5 * 5 * 5 * 4 * 4, window fused into the first stage ----
+        // (the twiddle base is laundered per column so the compiler does not hoist
+        // hundreds of loop-invariant 64-bit table addresses out of the column loop)
+        const float2* twl = tw;
+        int ln = lane;
+        asm volatile("" : "+s"(twl), "+v"(ln));
+        wstage<5, 1, true>(z, twl, ln);
+        wstage<5, 5, false>(z, twl, ln);
+        wstage<5, 25, false>(z, twl, ln);
+        wstage<4, 125, false>(z, twl, ln);
+        wstage<4, 500, false>(z, twl, ln);
+        // ---- unpack X_k = (Z_k + conj Z_-k)/2 - i/2 W^k (Z_k - conj Z_-k), |X_k|^2 ----
+#pragma unroll
+        for (int i = 0; i < kLaneBins; ++i) {
+            if ((i & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+            const int k = ln + 64 * i;
+            if (k < kBins) {
+                const float2 Zk = z[k == kFFT ? 0 : k];
+                const float2 Zc = z[k == 0 ? 0 : kFFT - k];
+                const float er = 0.5f * (Zk.x + Zc.x), ei = 0.5f * (Zk.y - Zc.y);
+                const float dr = Zk.x - Zc.x, di = Zk.y + Zc.y;
+                const float2 W = twl[k];
+                const float pr = W.x * dr - W.y * di, pi = W.x * di + W.y * dr;
+                const float xr = er + 0.5f * pi, xi = ei - 0.5f * pr;
+                acc[i] += xr * xr + xi * xi;
+            }
+        }
+        wave_sync();  // the next column overwrites z
+    }
+    // ---- combine the waves (fp64) into the simulation's accumulator row (single writer) ----
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [kWv][kBins]
+#pragma unroll
+    for (int i = 0; i < kLaneBins; ++i) {
+        const int k = lane + 64 * i;
+        if (k < kBins) red[w * kBins + k] = acc[i];
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < kBins; k += kWv * 64) {
+        double sacc = 0.0;
+#pragma unroll
+        for (int v = 0; v < kWv; ++v) sacc += (double)red[v * kBins + k];
+        a.acc[(int64_t)b * kBins + k] += sacc;
+    }
+}
+
 // mean PSD (density scaling, one-sided) and the first argmax -> peak frequency
 __global__ void welch_peak_kernel(int B, int N, int nseg, double fs, const double* __restrict__ acc,
                                   double* __restrict__ peak, double* __restrict__ psd) {
@@ -255,7 +454,7 @@ __global__ void welch_peak_kernel(int B, int N, int nseg, double fs, const doubl
 
 extern "C" {
 
-size_t wc_welch_workspace_size(void) { return (size_t)kSeg * 2 * sizeof(double); }
+size_t wc_welch_workspace_size(void) { return (size_t)kSeg * 2 * sizeof(double) + (size_t)kSeg * sizeof(float2); }
 int wc_welch_bins(void) { return kBins; }
 
 int wc_welch_prepare(void* workspace, size_t ws_bytes, void* stream) {
@@ -282,11 +481,16 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
         if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
         hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
     } else {
-        const size_t lds = (size_t)2 * kG<float> * kFFT * sizeof(cx<float>) + 4 * kG<float> * sizeof(float);
-        hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<float>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
-        hipLaunchKernelGGL(welch_kernel<float>, dim3(B), dim3(kThreads), lds, st, a);
+        if (ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 && ld < INT32_MAX / 2) {
+            const size_t lds = (size_t)kWv * kFFT * sizeof(float2);  // 64,000 B
+            hipLaunchKernelGGL(welch_wave_kernel, dim3(B), dim3(kWv * 64), lds, st, a);
+        } else {  // unaligned rings (e.g. odd lengths): the LDS-Stockham kernel, scalar loads
+            const size_t lds = (size_t)2 * kG<float> * kFFT * sizeof(cx<float>) + 4 * kG<float> * sizeof(float);
+            hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<float>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
+            hipLaunchKernelGGL(welch_kernel<float>, dim3(B), dim3(kThreads), lds, st, a);
+        }
     }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
