@@ -159,7 +159,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32+f64acc" if args.precision == "f32" else "f64",
+        "dtype": "f32" if args.precision == "f32" else "f64",
         "data": "synthetic noise (Philox), real 90-node SC_opti_25julio connectome",
         "config": {"workload": "C3: full homogeneous (G,sigma) sweep x 50 seeds (whole_sweep_both.py) "
                                "per GPU, recorded phase tau_ip=2",

@@ -26,6 +26,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <algorithm>
 #include "wc_common.h"
 #include "wc_device.h"
 
@@ -119,8 +120,10 @@ enum : int {
     V_BF16X3 = 64,    // ablation: only the three leading terms (~2^-17 relative)
 };
 
-template <typename Real, int NT, int NW, int VAR, int MINW>
-__global__ void __launch_bounds__(NW * 64, MINW) wc_sde_kernel(const KArgs a) {
+// SG > 1: one workgroup holds SG groups of 16 simulations (SG x NW waves) that
+// share ONE LDS copy of the connectome image; each group has its own E exchange.
+template <typename Real, int NT, int NW, int VAR, int MINW, int SG = 1>
+__global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs a) {
     typedef typename Tr<Real>::acc_t acc_t;
     typedef __attribute__((ext_vector_type(4))) Real real4;
     static_assert(NT % NW == 0, "NW must divide NT");
@@ -140,14 +143,15 @@ __global__ void __launch_bounds__(NW * 64, MINW) wc_sde_kernel(const KArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [A-operand image, unless kFragRegs] [E exchange, 2 buffers, if NW > 1]
     const size_t frag_bytes = kFragRegs ? 0 : (size_t)kFragUnits * 64 * (kBf ? 16 : sizeof(real4));
+    const int grp = SG == 1 ? 0 : (threadIdx.x >> 6) / NW;
     char* xraw = smem + frag_bytes;
-    bf16x8* xb16 = reinterpret_cast<bf16x8*>(xraw);  // [2][NC][3][64]
-    real4* xbn = reinterpret_cast<real4*>(xraw);     // [2][NT][64]
+    bf16x8* xb16 = reinterpret_cast<bf16x8*>(xraw) + grp * (2 * NC * 3 * 64);  // [2][NC][3][64] per group
+    real4* xbn = reinterpret_cast<real4*>(xraw) + grp * (2 * NT * 64);         // [2][NT][64] per group
 
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
+    const int w = SG == 1 ? threadIdx.x >> 6 : (threadIdx.x >> 6) % NW;
     const int j = lane & 15, g = lane >> 4;
-    const int b = blockIdx.x * kSims + j;
+    const int b = (blockIdx.x * SG + grp) * kSims + j;
     const bool live = b < a.B;
     const int bb = live ? b : a.B - 1;  // tail lanes mirror the last sim, never store
     const int N = a.N;
@@ -421,7 +425,7 @@ __global__ void noise_kernel(const uint64_t* __restrict__ keys, int B, int N, in
 
 int tiles_for(int N) { return (N + 15) / 16; }
 
-template <typename Real, int NT, int NW, int VAR, int MINW = 1>
+template <typename Real, int NT, int NW, int VAR, int MINW = 1, int SG = 1>
 int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     constexpr bool bf = (VAR & (V_BF16X6 | V_BF16X3)) != 0;
     constexpr bool frag_regs = (VAR & V_FRAG_REGS) != 0;
@@ -430,21 +434,22 @@ int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
         const int total = NT * (NT / 2) * 64;
         hipLaunchKernelGGL((build_frag_bf16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
                            static_cast<bf16x8*>(ws));
-        lds = (frag_regs ? 0 : (size_t)NT * (NT / 2) * 3 * 64 * 16) + (NW > 1 ? (size_t)2 * (NT / 2) * 3 * 64 * 16 : 0);
+        lds = (frag_regs ? 0 : (size_t)NT * (NT / 2) * 3 * 64 * 16) +
+              (NW > 1 ? (size_t)SG * 2 * (NT / 2) * 3 * 64 * 16 : 0);
     } else {
         const int total = NT * NT * 64 * 4;
         hipLaunchKernelGGL((build_frag<Real, NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
                            static_cast<Real*>(ws));
         lds = (frag_regs ? 0 : (size_t)NT * NT * 64 * 4 * sizeof(Real)) +
-              (NW > 1 ? (size_t)2 * NT * 64 * 4 * sizeof(Real) : 0);
+              (NW > 1 ? (size_t)SG * 2 * NT * 64 * 4 * sizeof(Real) : 0);
     }
-    const int blocks = (ka.B + kSims - 1) / kSims;
-    auto kern = wc_sde_kernel<Real, NT, NW, VAR, MINW>;
+    const int blocks = (ka.B + kSims * SG - 1) / (kSims * SG);
+    auto kern = wc_sde_kernel<Real, NT, NW, VAR, MINW, SG>;
     if (lds > 65536) {
         hipError_t ea = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
     }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(NW * 64), lds, st, ka);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(NW * 64 * SG), lds, st, ka);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
     return WC_OK;
@@ -463,11 +468,36 @@ size_t frag_bytes(int N, int precision) {
     return (size_t)nt * (nt / 2) * 3 * 64 * 16;
 }
 
+int cu_count() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+        return 256;
+    return n;
+}
+
+// 81 <= N <= 96 (NT = 6).  Few groups of 16 sims: the register-resident product
+// kernel (connectome fragments in VGPRs, 214 registers, 2 workgroups per CU).
+// Many groups: ONE workgroup per CU holding SG = ceil(groups / CUs) groups that
+// share the LDS connectome image (<= 155 / 128 registers): every simulation is
+// resident at once (a single round of workgroups, no tail) at 3-4 waves/SIMD.
+int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+    constexpr int V = V_BF16X6 | V_KAHAN_A;
+    const int groups = (ka.B + kSims - 1) / kSims;
+    const int cus = cu_count();
+    if (groups <= 2 * cus) return launch_v<float, 6, 3, kVarF32>(ka, sc, ws, st);
+    switch (std::min(5, (groups + cus - 1) / cus)) {
+        case 3: return launch_v<float, 6, 3, V, 1, 3>(ka, sc, ws, st);
+        case 4: return launch_v<float, 6, 3, V, 1, 4>(ka, sc, ws, st);
+        default: return launch_v<float, 6, 3, V, 1, 5>(ka, sc, ws, st);
+    }
+}
+
 int launch_f32(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     switch ((tiles_for(ka.N) + 1) & ~1) {
         case 2: return launch_v<float, 2, 1, kVarF32>(ka, sc, ws, st);
         case 4: return launch_v<float, 4, 2, kVarF32>(ka, sc, ws, st);
-        case 6: return launch_v<float, 6, 3, kVarF32>(ka, sc, ws, st);
+        case 6: return launch_f32_nt6(ka, sc, ws, st);
         default: return wc_set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
     }
 }
@@ -503,6 +533,12 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 12: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS | K | V_NO_MFMA>(ka, sc, ws, st);
         case 13: return launch_v<float, 6, 3, V_BF16X3 | V_FRAG_REGS | K>(ka, sc, ws, st);
         case 14: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS>(ka, sc, ws, st);  // fp64 a_ie
+        // one workgroup per CU: SG groups of 16 sims share the LDS connectome image
+        case 15: return launch_v<float, 6, 3, V_BF16X6 | K, 1, 5>(ka, sc, ws, st);
+        case 16: return launch_v<float, 6, 3, V_BF16X6 | K, 1, 4>(ka, sc, ws, st);
+        case 17: return launch_v<float, 6, 3, V_BF16X6 | K, 1, 3>(ka, sc, ws, st);
+        case 18: return launch_v<float, 6, 2, V_BF16X6 | K, 1, 5>(ka, sc, ws, st);
+        case 19: return launch_v<float, 6, 6, V_BF16X6 | K, 1, 2>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }

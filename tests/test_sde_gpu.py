@@ -148,3 +148,30 @@ def test_f32_tracks_f64_statistics(cuda, sc90):
         b.integrate(50_000, 2.0, 20, rec)
         out[prec] = rec.double().mean(0).cpu().numpy()
     assert np.abs(out["f32"] - out["f64"]).max() < 0.02
+
+
+@pytest.mark.parametrize("B", [9000, 20000])
+def test_grouped_kernel_matches_register_kernel(cuda, sc90, B):
+    """Large batches run the one-workgroup-per-CU kernel (SG groups of 16 sims
+    sharing the LDS connectome image); its trajectories equal the register-
+    resident kernel's (small batch, same keys) bit for bit, and the oracle's
+    within the fp32 tolerance."""
+    rng = np.random.default_rng(B)
+    G = 0.16 + rng.uniform(-0.1, 0.3, B)
+    S = 7.68 + rng.uniform(-0.2, 0.2, B)
+    keys = sim_keys(np.arange(B) % 50, np.arange(B) // 50)
+    big = Batch(sc90, G, S, keys, precision="f32")
+    small = Batch(sc90, G[:40], S[:40], keys[:40], precision="f32")
+    rb = torch.empty((15, B, 90), dtype=torch.float32, device="cuda")
+    rs = torch.empty((15, 40, 90), dtype=torch.float32, device="cuda")
+    for bt, r in ((big, rb), (small, rs)):
+        bt.integrate(100, 0.05)
+        bt.integrate(300, 2.0, 20, r)
+    torch.cuda.synchronize()
+    assert torch.equal(rb[:, :40], rs)
+    assert torch.equal(big.E[:40], small.E) and torch.equal(big.A[:40], small.A)
+    ob = oracle.OracleBatch(sc90, G[-24:], S[-24:], keys[-24:], driver_params())
+    ob.integrate(100, 0.05)
+    o = ob.integrate(300, 2.0, 20)
+    d = np.abs(rb[:, -24:].double().cpu().numpy().transpose(1, 0, 2) - o)
+    assert d.max() <= 2e-3 and np.sqrt(np.mean(d ** 2)) <= 2e-4
