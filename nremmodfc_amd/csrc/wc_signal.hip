@@ -11,15 +11,17 @@
 // trajectory array is time-major [t][C] so consecutive threads read
 // consecutive addresses at every time step (HBM-coalesced).
 //
-// filtfilt without the trajectory (DESIGN.md "Kernel 2"): the forward IIR is
-// causal and streams with the BOLD ODE.  The backward IIR is linear, so over a
+// filtfilt without the trajectory: the forward IIR is causal
+// and streams with the BOLD ODE.  The backward IIR is linear, so over a
 // decimation block of L samples its state obeys z_out = A^L z_in + u and the
-// decimated output is y_zs + c A^(L-1) z_in, where (y_zs, u) come from a zero-
-// state backward pass over the block alone.  wc_bold_chunk keeps one block of
-// forward output per column and emits (y_zs, u); wc_bold_finish runs the
-// 298-step backward recursion over blocks from the end state of the
-// odd-extended tail -- exactly filtfilt's result, never holding more than one
-// block of samples.
+// decimated output is y_zs + c A^(L-1) z_in, where (y_zs, u) -- the zero-state
+// backward pass over the block alone -- are fixed linear functionals of the
+// block: y_zs = sum_k h[k] y[k], u = sum_k G[k] y[k], with h / G the filter's
+// impulse response / state response at lag k (position k from the block
+// START: independent of the block length).  wc_bold_init tabulates (h, G) in
+// double-double; wc_bold_chunk accumulates the five sums as the forward output
+// is produced (no block buffer at all); wc_bold_finish runs the 298-step
+// backward recursion over blocks from the end state of the odd-extended tail.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -34,20 +36,21 @@ namespace {
 
 constexpr int kPad = 15;  // filtfilt padlen = 3*max(len(a), len(b)) for an order-4 filter
 
-// state layout (doubles), all [k][C] planes
+// state layout (doubles), all [k][C] planes, then the (h, G) table [dec][5]
 struct BoldLayout {
     int64_t C, M;
-    int64_t bal, zf, head, x16, ring, yzs, u, zend, total;
+    int64_t bal, zf, head, x16, acc, yzs, u, zend, tab, total;
     __host__ __device__ BoldLayout(int64_t C_, int64_t M_, int64_t dec) : C(C_), M(M_) {
         bal = 0;                 // 4: s, f, v, q
         zf = bal + 4 * C;        // 4: forward IIR state
         head = zf + 4 * C;       // 16: x[0..15]
         x16 = head + 16 * C;     // 16: x[n-16..n-1]
-        ring = x16 + 16 * C;     // dec: forward output of the current block
-        yzs = ring + dec * C;    // M: zero-state backward output at each block start
+        acc = x16 + 16 * C;      // 5: running (y_zs, u) sums of the current block
+        yzs = acc + 5 * C;       // M: zero-state backward output at each block start
         u = yzs + M * C;         // 4M: zero-state backward state after each block
         zend = u + 4 * M * C;    // 4: backward state entering the last sample
-        total = zend + 4 * C;
+        tab = zend + 4 * C;      // dec x 5: h[k], G[k][0..3]
+        total = tab + 5 * dec;
     }
 };
 
@@ -67,57 +70,69 @@ __device__ __forceinline__ double iir_step(double z[4], double x, const double* 
 struct BoldArgs {
     wc_bold_cfg cfg;
     int64_t C, n, M;
-    double itaus, itauf, itauo, ialpha, Eo, vo, k1, k2, k3, log1mEo;
+    double itaus, itauf, itauo, ialpha, iEo, vo, k1, k2, k3, log1mEo;
+    int alpha_3125;  // 1/alpha == 3.125: v^(1/alpha) = v^3 * v^(1/8) by square roots
 };
 
-// zero-state backward pass over one block of forward output held in the ring
-__device__ __forceinline__ void process_block(const BoldArgs& a, const BoldLayout& L, double* st, int64_t c,
-                                              int64_t m, int64_t len) {
-    double z[4] = {0, 0, 0, 0};
-    double yzs = 0;
-    for (int64_t kk = len - 1; kk >= 0; --kk) {
-        const double y = st[L.ring + kk * L.C + c];
-        yzs = iir_step(z, y, a.cfg.b, a.cfg.a);
-    }
-    st[L.yzs + m * L.C + c] = yzs;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) st[L.u + (m * 4 + k) * L.C + c] = z[k];
-}
-
+// forward output y of data sample k: accumulate the block's zero-state backward
+// summaries; at the block's last sample store them (block m = k / dec)
 __device__ __forceinline__ void emit(const BoldArgs& a, const BoldLayout& L, double* st, int64_t c, int64_t k,
-                                     double y) {
+                                     double y, double acc[5]) {
     const int64_t dec = a.cfg.dec;
     const int64_t r = k % dec;
-    st[L.ring + r * L.C + c] = y;
-    if (r == dec - 1 || k == a.n - 1) process_block(a, L, st, c, k / dec, r + 1);
+    const double* tab = st + L.tab + 5 * r;  // wave-uniform address: scalar loads
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[j] += tab[j] * y;
+    if (r == dec - 1 || k == a.n - 1) {
+        const int64_t m = k / dec;
+        st[L.yzs + m * L.C + c] = acc[0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st[L.u + (m * 4 + j) * L.C + c] = acc[1 + j];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[j] = 0.0;
+    }
 }
 
 // E layout: e_ld == 0 -> time-major [Tc][C]; e_ld > 0 -> node-major, sample tt of
 // column c at c*e_ld + tt (a slot of the integrator's recording ring)
+// One thread per column.  The lane-per-column walk of a node-major ring touches
+// 64 cache lines per load, but each line serves 16 consecutive samples from L1;
+// staging tiles through LDS for coalescing measured 10% SLOWER (the kernel is
+// bound by its fp64 Balloon arithmetic, not by these loads).
 template <typename ET>
-__global__ void bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, int64_t e_ld, int64_t t0, int64_t Tc,
-                                  double* __restrict__ st) {
+__global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, int64_t e_ld,
+                                                         int64_t t0, int64_t Tc, double* __restrict__ st) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= a.C) return;
+    const int64_t cc = c;
     const BoldLayout L(a.C, a.M, a.cfg.dec);
     const double* b = a.cfg.b;
     const double* fa = a.cfg.a;
-    double s = st[L.bal + c], f = st[L.bal + a.C + c], v = st[L.bal + 2 * a.C + c], q = st[L.bal + 3 * a.C + c];
-    double zf[4];
+    double s = st[L.bal + cc], f = st[L.bal + a.C + cc], v = st[L.bal + 2 * a.C + cc], q = st[L.bal + 3 * a.C + cc];
+    double zf[4], acc[5];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) zf[k] = st[L.zf + k * a.C + c];
+    for (int k = 0; k < 4; ++k) zf[k] = st[L.zf + k * a.C + cc];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) acc[k] = st[L.acc + k * a.C + cc];
     const int64_t neq = a.cfg.neq, n = a.n;
     const double dt = a.cfg.dt;
     for (int64_t tt = 0; tt < Tc; ++tt) {
         const int64_t t = t0 + tt;
-        // Balloon-Windkessel: BOLD[t] from the state after t steps (see oracle/wc_oracle.c orc_bold)
-        const double bold = a.vo * (a.k1 * (1.0 - q) + a.k2 * (1.0 - q / v) + a.k3 * (1.0 - v));
         const double x = (double)E[e_ld ? c * e_ld + tt : tt * a.C + c];
-        const double vpow = exp(log(v) * a.ialpha);
+        // Balloon-Windkessel: BOLD[t] from the state after t steps (see oracle/wc_oracle.c orc_bold)
+        const double iv = 1.0 / v;
+        const double bold = a.vo * (a.k1 * (1.0 - q) + a.k2 * (1.0 - q * iv) + a.k3 * (1.0 - v));
+        double vpow;
+        if (a.alpha_3125) {
+            const double r8 = sqrt(sqrt(sqrt(v)));
+            vpow = v * v * v * r8;
+        } else {
+            vpow = exp(log(v) * a.ialpha);
+        }
         const double fpow = exp(a.log1mEo / f);
         const double ds = x - a.itaus * s - a.itauf * (f - 1.0);
         const double dv = (f - vpow) * a.itauo;
-        const double dq = (f * (1.0 - fpow) / a.Eo - q * vpow / v) * a.itauo;
+        const double dq = (f * (1.0 - fpow) * a.iEo - q * vpow * iv) * a.itauo;
         const double df = s;
         s += dt * ds;
         f += dt * df;
@@ -136,9 +151,9 @@ __global__ void bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, in
 #pragma unroll
             for (int k = 0; k < 4; ++k) zf[k] = a.cfg.zi[k] * e0;
             for (int k = 15; k >= 1; --k) iir_step(zf, 2.0 * x0 - st[L.head + k * a.C + c], b, fa);
-            for (int k = 0; k <= 15; ++k) emit(a, L, st, c, k, iir_step(zf, st[L.head + k * a.C + c], b, fa));
+            for (int k = 0; k <= 15; ++k) emit(a, L, st, c, k, iir_step(zf, st[L.head + k * a.C + c], b, fa), acc);
         } else {
-            emit(a, L, st, c, i, iir_step(zf, bold, b, fa));
+            emit(a, L, st, c, i, iir_step(zf, bold, b, fa), acc);
         }
         if (i == n - 1) {
             // odd extension at the end: 2 x[n-1] - x[n-2..n-16]; backward pass starts there
@@ -161,6 +176,8 @@ __global__ void bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, in
     st[L.bal + 3 * a.C + c] = q;
 #pragma unroll
     for (int k = 0; k < 4; ++k) st[L.zf + k * a.C + c] = zf[k];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) st[L.acc + k * a.C + c] = acc[k];
 }
 
 __global__ void bold_init_kernel(int64_t C, double* st) {
@@ -172,6 +189,9 @@ __global__ void bold_init_kernel(int64_t C, double* st) {
     st[3 * C + c] = 1.0;  // q
 #pragma unroll
     for (int k = 0; k < 4; ++k) st[4 * C + k * C + c] = 0.0;
+    const BoldLayout L(C, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) st[L.acc + k * C + c] = 0.0;
 }
 
 // ---- block combination in the filter's modal basis, double-double ----
@@ -216,6 +236,23 @@ __host__ __device__ inline cdd cdd_mul(cdd a, cdd b) {
     return {dd_add(dd_mul(a.re, b.re), dd_neg(dd_mul(a.im, b.im))), dd_add(dd_mul(a.re, b.im), dd_mul(a.im, b.re))};
 }
 __host__ __device__ inline cdd cdd_add(cdd a, cdd b) { return {dd_add(a.re, b.re), dd_add(a.im, b.im)}; }
+
+// (h, G) table of the backward zero-state pass: DF2T impulse response h[k] and
+// state G[k] after k zero steps following a unit impulse, in double-double (one thread)
+__global__ void bold_table_kernel(const wc_bold_cfg cfg, double* tab) {
+    dd z[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+    for (int64_t k = 0; k < cfg.dec; ++k) {
+        const double x = k == 0 ? 1.0 : 0.0;
+        const dd y = dd_add(z[0], {x * cfg.b[0], 0.0});
+        z[0] = dd_add(dd_add(z[1], {x * cfg.b[1], 0.0}), dd_neg(dd_mul_d(y, cfg.a[1])));
+        z[1] = dd_add(dd_add(z[2], {x * cfg.b[2], 0.0}), dd_neg(dd_mul_d(y, cfg.a[2])));
+        z[2] = dd_add(dd_add(z[3], {x * cfg.b[3], 0.0}), dd_neg(dd_mul_d(y, cfg.a[3])));
+        z[3] = dd_add({x * cfg.b[4], 0.0}, dd_neg(dd_mul_d(y, cfg.a[4])));
+        tab[5 * k] = y.hi + y.lo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tab[5 * k + 1 + j] = z[j].hi + z[j].lo;
+    }
+}
 __host__ __device__ inline cdd cdd_mul_d(cdd a, double d) { return {dd_mul_d(a.re, d), dd_mul_d(a.im, d)}; }
 #pragma clang fp contract(on)
 
@@ -668,12 +705,14 @@ BoldArgs make_bold_args(const wc_bold_cfg* cfg, int64_t C) {
     a.itauf = 1.0 / 0.41;
     a.itauo = 1.0 / 0.98;
     a.ialpha = 1.0 / 0.32;
-    a.Eo = 0.4;
+    a.alpha_3125 = a.ialpha == 3.125;
+    a.iEo = 1.0 / 0.4;
     a.vo = 0.04;
-    a.k1 = 7.0 * a.Eo;
+    const double Eo = 0.4;
+    a.k1 = 7.0 * Eo;
     a.k2 = 2.0;
-    a.k3 = 2.0 * a.Eo - 0.2;
-    a.log1mEo = log(1.0 - a.Eo);
+    a.k3 = 2.0 * Eo - 0.2;
+    a.log1mEo = log(1.0 - Eo);
     return a;
 }
 
@@ -698,6 +737,9 @@ int wc_bold_init(const wc_bold_cfg* cfg, int64_t C, double* state, void* stream)
     if (!state) return wc_set_err(WC_EINVAL, "wc_bold_init: NULL state");
     hipLaunchKernelGGL(bold_init_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0,
                        static_cast<hipStream_t>(stream), C, state);
+    const BoldLayout L(C, wc_bold_blocks(cfg), cfg->dec);
+    hipLaunchKernelGGL(bold_table_kernel, dim3(1), dim3(1), 0, static_cast<hipStream_t>(stream), *cfg,
+                       state + L.tab);
     return wc_hip_check("wc_bold_init");
 }
 
