@@ -5,9 +5,12 @@ Workload (BASELINE.json configs[2], the metric's config, one GPU): the full
 homogeneous sweep of whole_sweep_both.py -- 50 seeds x 20 dG x 20 dsigma =
 20,000 simulations of the 90-node AAL connectome (SC_opti_25julio), G = 0.16 +
 dG, sigmaE = 7.68 + dsigma on the shipped grid (whole_sweep_both_maps.py:92-93).
-One bench "step" = one chunk of `--chunk` Euler steps of the recorded phase
-(tau_ip = 2, E stored every 20 steps, wc:118-135) for every simulation of the
-batch, state and inputs resident in HBM.  With --gpus N (torchrun, one rank per
+One bench "step" = 2000 recorded samples of every simulation of the batch: two
+chunks of 20,000 Euler steps of the recorded phase (tau_ip = 2, E stored every
+20 steps into the 4-slot ring, wc:118-135), each followed by the streamed
+BOLD / band-pass stage, plus one 4000-sample Welch segment -- the steady state of
+the sweep pipeline (nremmodfc_amd/pipeline.py); inputs and state resident in
+HBM.  --sde-only times the integrator alone.  With --gpus N (torchrun, one rank per
 GPU) each rank runs its own 20,000-simulation shard (seeds 50r..50r+49):
 weak scaling, no data-path collective.
 
@@ -80,8 +83,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--chunk", type=int, default=10_000, help="Euler steps per bench step")
     ap.add_argument("--precision", default="f32", choices=("f32", "f64"))
+    ap.add_argument("--config", default="c3", choices=("c3", "c5"),
+                    help="c3: 20,000 sims x 90 nodes per GPU (the metric's config); c5: the 1000-node "
+                         "synthetic connectome, 2,500 sims per GPU (20,000 over 8 GPUs)")
+    ap.add_argument("--sde-only", action="store_true",
+                    help="time the integrator alone (no streamed BOLD / Welch consumers)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -95,20 +102,58 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    sc = datasets.load_sc()
+    from nremmodfc_amd.sigchain import NEQ, BoldStream, WelchAccumulator
+
+    if args.config == "c5":
+        sc = datasets.synthetic_sc(1000)
+        G, S, keys = sweep_batch(rank)
+        lo = rank * 2500 % len(keys)
+        G, S, keys = G[lo:lo + 2500], S[lo:lo + 2500], keys[lo:lo + 2500]
+    else:
+        sc = datasets.load_sc()
+        G, S, keys = sweep_batch(rank)
     N = sc.shape[0]
-    G, S, keys = sweep_batch(rank)
     B = len(keys)
+    C = B * N
     p = driver_params()
-    bt = Batch(sc, G, S, keys, p, precision=args.precision, device=f"cuda:{local}")
-    R = 20
-    n_rec = -(-args.chunk // R)
-    rec = torch.empty((n_rec, B, N), dtype=bt.rec_dtype, device=bt.device)
-    # reach the recorded phase's operating point cheaply: a short transient
-    bt.integrate(2000, 0.05)
+    dev = torch.device("cuda", local)
+    bt = Batch(sc, G, S, keys, p, precision=args.precision, device=dev)
+    R, CH, NSLOT = 20, 1000, 4           # record every 20 steps; 1000-sample chunks; 4-slot ring
+    LD = CH * NSLOT
+    EULER = CH * R                       # Euler steps per chunk
+    CHUNKS = 2                           # chunks per bench step (one Welch segment per step)
+    n_total = (args.warmup + args.steps) * CHUNKS * CH + NEQ
+    ring = torch.empty(C * LD, dtype=bt.rec_dtype, device=dev)
+    bold = welch = None
+    if not args.sde_only:
+        bold = BoldStream(C, max(n_total, 300_000), NEQ, 1000, p.dt * p.downsamp, dev)
+        welch = WelchAccumulator(B, N, dev)
+    # (no separate transient launch: every wc_sde_kernel launch of the run is one 20,000-step chunk,
+    # so the rocprofv3 average of the kernel equals the per-launch time reported here)
+    state = {"k": 0, "timed": False}
+    ev = {"sde": [], "bold": [], "welch": []}
+
+    def timed(name, fn):
+        if not state["timed"]:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        ev[name].append((e0, e1))
 
     def step():
-        bt.integrate(args.chunk, 2.0, R, rec)
+        """2000 recorded samples (40,000 Euler steps) of every simulation: integrate into the ring,
+        stream BOLD over each 1000-sample chunk, one 4000-sample Welch segment."""
+        for _ in range(CHUNKS):
+            k = state["k"]
+            slot = k % NSLOT
+            timed("sde", lambda: bt.integrate(EULER, 2.0, R, ring[slot * CH:], rec_ld=LD))
+            if bold is not None:
+                timed("bold", lambda: bold.feed(ring, CH, e_ld=LD, offset=slot * CH))
+            state["k"] = k = k + 1
+            if welch is not None and k >= NSLOT and k % 2 == 0:
+                timed("welch", lambda: welch.accumulate(ring, LD, CH, NSLOT, (k - NSLOT) * CH))
 
     for _ in range(args.warmup):
         step()
@@ -116,40 +161,39 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    state["timed"] = True
     t0 = time.perf_counter()
-    ev0.record()
     for _ in range(args.steps):
         step()
-    ev1.record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # device time per launch pair (prep + SDE kernel)
     if dist:
-        t = torch.tensor([elapsed], device=bt.device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    node_steps = B * N * args.chunk * args.steps * world
+    kern = {k: (sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None) for k, v in ev.items()}
+    node_steps = B * N * EULER * CHUNKS * args.steps * world
     value = node_steps / elapsed
-    per_launch_ns = B * N * args.chunk
     fl = flops_per_node_step(N)
     peak = PEAK_FP32_TFLOPS if args.precision == "f32" else PEAK_FP64_TFLOPS
-    achieved = per_launch_ns * fl / (kern_ms * 1e-3) / 1e12
+    per_launch_ns = B * N * EULER
+    achieved = per_launch_ns * fl / (kern["sde"] * 1e-3) / 1e12
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_sde.json")
     if os.path.exists(pmc):
         try:
             d = json.load(open(pmc))
-            if d.get("B") == B and d.get("N") == N and d.get("chunk") == args.chunk and \
+            if d.get("B") == B and d.get("N") == N and d.get("euler_steps") == EULER and \
                     d.get("precision") == args.precision:
                 traffic = d.get("hbm_bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
     out = {
-        "metric": "node-timesteps/sec (90-node WC, (G,sigma)x50-seed sweep) at 1/2/4/8 GPUs",
+        "metric": "node-timesteps/sec (90-node WC, (G,sigma)x50-seed sweep) at 1/2/4/8 GPUs"
+                  + ("" if args.config == "c3" else " [config 5: 1000-node synthetic connectome]"),
         "value": value,
         "unit": "node-timesteps/sec",
         "n_gpus": world,
@@ -160,17 +204,26 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32" if args.precision == "f32" else "f64",
-        "data": "synthetic noise (Philox), real 90-node SC_opti_25julio connectome",
-        "config": {"workload": "C3: full homogeneous (G,sigma) sweep x 50 seeds (whole_sweep_both.py) "
-                               "per GPU, recorded phase tau_ip=2",
-                   "sims_per_gpu": B, "nodes": N, "euler_steps_per_step": args.chunk,
+        "data": "synthetic noise (Philox), " + ("real 90-node SC_opti_25julio connectome" if args.config == "c3"
+                                                else "synthetic 1000-node connectome (datasets.synthetic_sc)"),
+        "config": {"workload": ("C3: full homogeneous (G,sigma) sweep x 50 seeds (whole_sweep_both.py) per GPU; "
+                                if args.config == "c3" else
+                                "C5: 1000-node synthetic connectome, 2,500 sims of the (G,sigma) grid per GPU; ")
+                               + "one step = 2000 recorded samples (40,000 Euler steps, tau_ip=2) of every simulation"
+                               + ("" if args.sde_only else
+                                  " + streamed BOLD/band-pass of both 1000-sample chunks + one Welch segment"),
+                   "sims_per_gpu": B, "nodes": N, "euler_steps_per_step": EULER * CHUNKS,
                    "record_every": R, "parallelism": f"sims sharded x{world}"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": traffic,
-                     "kernel_ms_per_launch": kern_ms,
+                     "traffic_algorithmic": B * N * (EULER // R * 4 + 2 * 3 * 8 + 2 * 8),
+                     "kernel": ("wc_sde_kernel (one launch = %d Euler steps of %d sims)" % (EULER, B) if N <= 96 else
+                                "step_kernel (wc_sde_large.hip; %d launches of 1 Euler step, %d sims)" % (EULER, B)),
+                     "kernel_ms_per_launch": kern["sde"],
                      "flops_per_node_step": fl},
+        "kernel_ms": kern,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         out["cpu_baseline"] = cpu_baseline(sc, seconds=args.cpu_seconds)
     elif rank == 0:
         out["cpu_baseline"] = None

@@ -69,7 +69,8 @@ def main():
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            diag(bt, v, steps, 2.0, 20, rec)
+            rec_every = int(os.environ.get("DIAG_REC", "20"))
+            diag(bt, v, steps, 2.0, rec_every, rec if rec_every else None)
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1))
