@@ -118,6 +118,8 @@ enum : int {
     V_KAHAN_A = 8,    // fp32: a_ie as a compensated fp32 pair instead of fp64
     V_BF16X6 = 32,    // fp32 coupling as the six bf16 cross terms (product)
     V_BF16X3 = 64,    // ablation: only the three leading terms (~2^-17 relative)
+    V_REC2 = 128,     // node-major E records buffered 2 deep: one 8-B store per node per 2 records
+    V_REC4 = 256,     // ... 4 deep: one 16-B store per node per 4 records (host checks eligibility)
 };
 
 // SG > 1: one workgroup holds SG groups of 16 simulations (SG x NW waves) that
@@ -263,13 +265,48 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     const size_t BN = (size_t)a.B * N;
     const int rec_every = (int)a.rec_every;
     int rec_cnt = 0, rec_row = 0;
+    // record buffer (RB > 1): the RB-1 previous E records of this lane's nodes, oldest first
+    constexpr int RB = (VAR & V_REC4) ? 4 : (VAR & V_REC2) ? 2 : 1;
+    Real rbuf[RB > 1 ? OT : 1][4][RB > 1 ? RB - 1 : 1];
 
     for (int s = 0; s < a.nsteps; ++s) {
         const int buf = s & 1;
         // ---- record the state before the update (wc:124-125) ----
         if (rec_every > 0) {
             if (rec_cnt == 0) {
-                if (live) {
+                if constexpr (RB > 1) {
+                    // node-major ring, E only: flush RB records as one vector store per node
+                    if (rec_row % RB == RB - 1) {
+                        if (live) {
+#pragma unroll
+                            for (int u = 0; u < OT; ++u)
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    const int n = 16 * (T0 + u) + 4 * g + r;
+                                    if (n < N) {
+                                        Real* dst = static_cast<Real*>(a.recE) + ((size_t)bb * N + n) * a.rec_ld +
+                                                    (rec_row - (RB - 1));
+                                        if constexpr (RB == 4) {
+                                            *reinterpret_cast<real4*>(dst) =
+                                                real4{rbuf[u][r][0], rbuf[u][r][1], rbuf[u][r][2], E[u][r]};
+                                        } else {
+                                            typedef __attribute__((ext_vector_type(2))) Real real2;
+                                            *reinterpret_cast<real2*>(dst) = real2{rbuf[u][r][0], E[u][r]};
+                                        }
+                                    }
+                                }
+                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < OT; ++u)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+#pragma unroll
+                                for (int k = 0; k + 1 < RB - 1; ++k) rbuf[u][r][k] = rbuf[u][r][k + 1];
+                                rbuf[u][r][RB - 2] = E[u][r];
+                            }
+                    }
+                } else if (live) {
 #pragma unroll
                     for (int u = 0; u < OT; ++u)
 #pragma unroll
@@ -394,6 +431,24 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         publish(buf ^ 1);
     }
 
+    // ---- records still buffered (rec_row % RB of them): the newest are the last rbuf slots ----
+    if constexpr (RB > 1) {
+        const int m = rec_row % RB;
+        if (rec_every > 0 && m > 0 && live) {
+#pragma unroll
+            for (int u = 0; u < OT; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = 16 * (T0 + u) + 4 * g + r;
+                    if (n < N) {
+                        Real* dst = static_cast<Real*>(a.recE) + ((size_t)bb * N + n) * a.rec_ld + (rec_row - m);
+#pragma unroll
+                        for (int k = 0; k < RB - 1; ++k)
+                            if (k < m) dst[k] = rbuf[u][r][RB - 1 - m + k];
+                    }
+                }
+        }
+    }
     // ---- write back the state (own tiles) ----
     if (live) {
 #pragma unroll
@@ -486,10 +541,14 @@ int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) 
     const int groups = (ka.B + kSims - 1) / kSims;
     const int cus = cu_count();
     if (groups <= 2 * cus) return launch_v<float, 6, 3, kVarF32>(ka, sc, ws, st);
+    // node-major E-only recording (the sweep pipeline's ring): pairs of records per 8-B store
+    const bool rec2 = ka.rec_every > 0 && ka.rec_ld > 0 && ka.rec_ld % 2 == 0 && !ka.recI && !ka.recA &&
+                      ((uintptr_t)ka.recE & 7) == 0;
+    constexpr int V2 = V | V_REC2;
     switch (std::min(5, (groups + cus - 1) / cus)) {
-        case 3: return launch_v<float, 6, 3, V, 1, 3>(ka, sc, ws, st);
-        case 4: return launch_v<float, 6, 3, V, 1, 4>(ka, sc, ws, st);
-        default: return launch_v<float, 6, 3, V, 1, 5>(ka, sc, ws, st);
+        case 3: return rec2 ? launch_v<float, 6, 3, V2, 1, 3>(ka, sc, ws, st) : launch_v<float, 6, 3, V, 1, 3>(ka, sc, ws, st);
+        case 4: return rec2 ? launch_v<float, 6, 3, V2, 1, 4>(ka, sc, ws, st) : launch_v<float, 6, 3, V, 1, 4>(ka, sc, ws, st);
+        default: return rec2 ? launch_v<float, 6, 3, V2, 1, 5>(ka, sc, ws, st) : launch_v<float, 6, 3, V, 1, 5>(ka, sc, ws, st);
     }
 }
 
@@ -539,6 +598,11 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 17: return launch_v<float, 6, 3, V_BF16X6 | K, 1, 3>(ka, sc, ws, st);
         case 18: return launch_v<float, 6, 2, V_BF16X6 | K, 1, 5>(ka, sc, ws, st);
         case 19: return launch_v<float, 6, 6, V_BF16X6 | K, 1, 2>(ka, sc, ws, st);
+        // node-major record buffering (needs rec_ld % 4 == 0, E records only)
+        case 20: return launch_v<float, 6, 3, V_BF16X6 | K | V_REC4, 1, 5>(ka, sc, ws, st);
+        case 21: return launch_v<float, 6, 3, V_BF16X6 | K | V_REC2, 1, 5>(ka, sc, ws, st);
+        case 22: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS | K | V_REC4>(ka, sc, ws, st);
+        case 23: return launch_v<float, 6, 3, V_BF16X6 | K, 1, 5>(ka, sc, ws, st);  // = 15, node-major records
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
@@ -607,7 +671,10 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
                       int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* workspace,
                       size_t ws_bytes, void* stream) {
     KArgs ka;
-    int rc = make_args(ka, p, WC_F32, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, 0,
+    // variants 20..22 record node-major into a dense [B*N][ld] buffer, ld = n_rec rounded up to 4
+    const int64_t n_rec = rec_every > 0 ? (nsteps + rec_every - 1) / rec_every : 0;
+    const int64_t ld = (variant >= 20 && variant < 100 && rec_every > 0) ? (n_rec + 3) & ~int64_t(3) : 0;
+    int rc = make_args(ka, p, WC_F32, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, ld,
                        recE, nullptr, nullptr, workspace, ws_bytes);
     if (rc != WC_OK || nsteps == 0) return rc;
     if (variant >= 100) {

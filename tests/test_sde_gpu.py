@@ -175,3 +175,28 @@ def test_grouped_kernel_matches_register_kernel(cuda, sc90, B):
     o = ob.integrate(300, 2.0, 20)
     d = np.abs(rb[:, -24:].double().cpu().numpy().transpose(1, 0, 2) - o)
     assert d.max() <= 2e-3 and np.sqrt(np.mean(d ** 2)) <= 2e-4
+
+
+@pytest.mark.parametrize("nsteps", [400, 380, 20])
+def test_grouped_kernel_ring_records(cuda, sc90, nsteps):
+    """The pipeline's node-major ring (rec_ld > 0) through the grouped kernel with
+    paired-record stores, including an odd record count (buffer flushed at exit):
+    equal to the time-major records of the same trajectory."""
+    B = 9000
+    rng = np.random.default_rng(7)
+    G = 0.16 + rng.uniform(-0.1, 0.3, B)
+    S = 7.68 + rng.uniform(-0.2, 0.2, B)
+    keys = sim_keys(np.arange(B) % 50, np.arange(B) // 50)
+    n_rec = -(-nsteps // 20)
+    a = Batch(sc90, G, S, keys, precision="f32")
+    b = Batch(sc90, G, S, keys, precision="f32")
+    tm = torch.empty((n_rec, B, 90), dtype=torch.float32, device="cuda")
+    ld = 32
+    ring = torch.full((B * 90 * ld,), float("nan"), dtype=torch.float32, device="cuda")
+    a.integrate(nsteps, 2.0, 20, tm)
+    b.integrate(nsteps, 2.0, 20, ring[4:], rec_ld=ld)
+    torch.cuda.synchronize()
+    nm = ring.view(B * 90, ld)[:, 4:4 + n_rec].reshape(B, 90, n_rec).permute(2, 0, 1)
+    assert torch.equal(nm, tm)
+    assert torch.isnan(ring.view(B * 90, ld)[:, 4 + n_rec:]).all()  # nothing written past the last record
+    assert torch.equal(a.E, b.E)

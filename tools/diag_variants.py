@@ -54,14 +54,21 @@ def main():
     for v in variants:
         bt = Batch(sc, sG, sS, sk, p, precision="f32")
         diag(bt, v, 300, 0.05)
-        rec = torch.empty((30, 37, 90), dtype=torch.float32, device="cuda")
-        diag(bt, v, 600, 2.0, 20, rec)
+        if 20 <= v < 100:  # node-major [B*N][32] records
+            rec = torch.empty((37 * 90, 32), dtype=torch.float32, device="cuda")
+            diag(bt, v, 600, 2.0, 20, rec)
+            got = rec[:, :30].reshape(37, 90, 30).permute(0, 2, 1)
+        else:
+            rec = torch.empty((30, 37, 90), dtype=torch.float32, device="cuda")
+            diag(bt, v, 600, 2.0, 20, rec)
+            got = rec.permute(1, 0, 2)
         torch.cuda.synchronize()
-        d = np.abs(rec.double().cpu().numpy().transpose(1, 0, 2) - orec)
+        d = np.abs(got.double().cpu().numpy() - orec)
         ok[v] = (float(d.max()), float(np.sqrt((d ** 2).mean())))
     # timing
     bt = Batch(sc, G, S, keys, p, precision="f32")
     rec = torch.empty((-(-steps // 20), bt.B, bt.N), dtype=torch.float32, device="cuda")
+    recn = torch.empty((bt.B * bt.N, (-(-steps // 20) + 3) // 4 * 4), dtype=torch.float32, device="cuda")
     diag(bt, variants[0], 500, 0.05)
     times = {v: [] for v in variants}
     for r in range(rounds):
@@ -70,7 +77,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             rec_every = int(os.environ.get("DIAG_REC", "20"))
-            diag(bt, v, steps, 2.0, rec_every, rec if rec_every else None)
+            diag(bt, v, steps, 2.0, rec_every, (recn if 20 <= v < 100 else rec) if rec_every else None)
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1))
