@@ -7,8 +7,9 @@ homogeneous sweep of whole_sweep_both.py -- 50 seeds x 20 dG x 20 dsigma =
 dG, sigmaE = 7.68 + dsigma on the shipped grid (whole_sweep_both_maps.py:92-93).
 One bench "step" = 2000 recorded samples of every simulation of the batch: two
 chunks of 20,000 Euler steps of the recorded phase (tau_ip = 2, E stored every
-20 steps into the 4-slot ring, wc:118-135), each followed by the streamed
-BOLD / band-pass stage, plus one 4000-sample Welch segment -- the steady state of
+20 steps, wc:118-135), each followed by the streamed BOLD / band-pass stage
+(which also transposes the chunk into the 4-slot Welch ring), plus one
+4000-sample Welch segment -- the steady state of
 the sweep pipeline (nremmodfc_amd/pipeline.py); inputs and state resident in
 HBM.  --sde-only times the integrator alone.  With --gpus N (torchrun, one rank per
 GPU) each rank runs its own 20,000-simulation shard (seeds 50r..50r+49):
@@ -124,6 +125,10 @@ def main():
     CHUNKS = 2                           # chunks per bench step (one Welch segment per step)
     n_total = (args.warmup + args.steps) * CHUNKS * CH + NEQ
     ring = torch.empty(C * LD, dtype=bt.rec_dtype, device=dev)
+    # fp32 + consumers: the integrator writes each chunk time-major, the BOLD pass transposes it
+    # into the node-major Welch ring (the sweep pipeline's layout, nremmodfc_amd/pipeline.py)
+    tmaj = torch.empty(CH * C, dtype=bt.rec_dtype, device=dev) \
+        if (args.precision == "f32" and not args.sde_only) else None
     bold = welch = None
     if not args.sde_only:
         bold = BoldStream(C, max(n_total, 300_000), NEQ, 1000, p.dt * p.downsamp, dev)
@@ -148,9 +153,13 @@ def main():
         for _ in range(CHUNKS):
             k = state["k"]
             slot = k % NSLOT
-            timed("sde", lambda: bt.integrate(EULER, 2.0, R, ring[slot * CH:], rec_ld=LD))
-            if bold is not None:
-                timed("bold", lambda: bold.feed(ring, CH, e_ld=LD, offset=slot * CH))
+            if tmaj is not None:
+                timed("sde", lambda: bt.integrate(EULER, 2.0, R, tmaj))
+                timed("bold", lambda: bold.feed(tmaj, CH, e_ld=0, copy=ring, copy_ld=LD, copy_offset=slot * CH))
+            else:
+                timed("sde", lambda: bt.integrate(EULER, 2.0, R, ring[slot * CH:], rec_ld=LD))
+                if bold is not None:
+                    timed("bold", lambda: bold.feed(ring, CH, e_ld=LD, offset=slot * CH))
             state["k"] = k = k + 1
             if welch is not None and k >= NSLOT and k % 2 == 0:
                 timed("welch", lambda: welch.accumulate(ring, LD, CH, NSLOT, (k - NSLOT) * CH))

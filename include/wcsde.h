@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define WCSDE_ABI_VERSION 2
+#define WCSDE_ABI_VERSION 3
 
 /* Noise stream (the reference's numba RNG is seeded from os.urandom and never
  * reproducible; the build defines its own): Philox4x32-10 with
@@ -136,9 +136,15 @@ int64_t wc_bold_blocks(const wc_bold_cfg* cfg);
 size_t wc_bold_state_doubles(const wc_bold_cfg* cfg, int64_t C);
 int wc_bold_init(const wc_bold_cfg* cfg, int64_t C, double* state, void* stream);
 /* E: float (e_f64 = 0) or double; e_ld == 0: time-major [Tc][C]; e_ld > 0:
- * node-major, sample tt of column c at E[c*e_ld + tt]. */
+ * node-major, sample tt of column c at E[c*e_ld + tt].
+ * copy (optional, fp32 time-major E only): the chunk is also written
+ * node-major, sample tt of column c at copy[c*copy_ld + tt] (copy_ld >= Tc;
+ * 16-B row stores when copy is 16-B aligned and copy_ld % 4 == 0) -- the
+ * transposition the Welch stage needs, done in the same pass as the BOLD
+ * stream through an LDS tile with full-line stores.
+ * NULL: no copy. */
 int wc_bold_chunk(const wc_bold_cfg* cfg, int64_t C, const void* E, int e_f64, int64_t e_ld,
-                  int64_t t0, int64_t Tc, double* state, void* stream);
+                  int64_t t0, int64_t Tc, double* state, void* copy, int64_t copy_ld, void* stream);
 int wc_bold_finish(const wc_bold_cfg* cfg, int64_t C, const double* state, double* out, void* stream);
 
 /* Unit phasors exp(i angle(hilbert(x, axis=0))) of every column of x [M][C]

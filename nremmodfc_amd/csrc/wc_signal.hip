@@ -95,20 +95,54 @@ __device__ __forceinline__ void emit(const BoldArgs& a, const BoldLayout& L, dou
 
 // E layout: e_ld == 0 -> time-major [Tc][C]; e_ld > 0 -> node-major, sample tt of
 // column c at c*e_ld + tt (a slot of the integrator's recording ring)
-// One thread per column.  The lane-per-column walk of a node-major ring touches
-// 64 cache lines per load, but each line serves 16 consecutive samples from L1;
-// staging tiles through LDS for coalescing measured 10% SLOWER (the kernel is
-// bound by its fp64 Balloon arithmetic, not by these loads).
-template <typename ET>
+// One thread per column (the kernel is bound by its fp64 Balloon arithmetic;
+// staging a node-major input through LDS for coalescing measured 10% slower).
+// COPY: time-major fp32 input, also written out node-major (copy[c*copy_ld + tt])
+// through a 256-column x 32-sample LDS tile flushed as 128-B rows.
+constexpr int kCopyT = 32;
+template <typename ET, bool COPY>
 __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, int64_t e_ld,
-                                                         int64_t t0, int64_t Tc, double* __restrict__ st) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.C) return;
-    const int64_t cc = c;
+                                                         int64_t t0, int64_t Tc, double* __restrict__ st,
+                                                         float* __restrict__ copy, int64_t copy_ld) {
+    const int64_t c0 = (int64_t)blockIdx.x * blockDim.x;
+    const int64_t c = c0 + threadIdx.x;
+    if (!COPY && c >= a.C) return;
+    const bool live = c < a.C;
+    const int64_t cc = live ? c : a.C - 1;  // COPY tail threads shadow the last column and never store
     const BoldLayout L(a.C, a.M, a.cfg.dec);
+    // per-wave tile (64 columns x 32 samples): each wave transposes its own columns,
+    // so the only synchronisation is the wave's own (no workgroup barrier)
+    __shared__ float tiles[COPY ? 4 * 64 * (kCopyT + 1) : 1];
+    float* tile = tiles + (threadIdx.x >> 6) * 64 * (kCopyT + 1);
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = c0 + (threadIdx.x & ~63);  // first column of this wave
+    // 16-B row stores when every row start is 16-B aligned, else scalar stores
+    const bool vec = COPY && ((uintptr_t)copy & 15) == 0 && copy_ld % 4 == 0;
+    // LDS operations of one wave complete in order: a compiler barrier plus an
+    // lgkmcnt drain orders the tile's writes and reads (a wavefront-scope release
+    // fence would also drain the in-flight row stores: 7 ms per chunk at C3)
+    auto wsync = []() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    auto flush = [&](int64_t tt0, int len) {  // tile samples [tt0, tt0+len) of the wave's columns
+        wsync();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int q = lane + 64 * i, col = q >> 3, part = q & 7;
+            if (w0 + col < a.C && 4 * part < len) {
+                const float* srow = tile + col * (kCopyT + 1) + 4 * part;
+                float* d = copy + (w0 + col) * copy_ld + tt0 + 4 * part;
+                if (vec && 4 * part + 4 <= len) {
+                    *reinterpret_cast<float4*>(d) = make_float4(srow[0], srow[1], srow[2], srow[3]);
+                } else {
+                    for (int k = 0; 4 * part + k < len; ++k) d[k] = srow[k];
+                }
+            }
+        }
+        wsync();
+    };
     const double* b = a.cfg.b;
     const double* fa = a.cfg.a;
     double s = st[L.bal + cc], f = st[L.bal + a.C + cc], v = st[L.bal + 2 * a.C + cc], q = st[L.bal + 3 * a.C + cc];
+    const int64_t ce = live ? c : a.C - 1;
     double zf[4], acc[5];
 #pragma unroll
     for (int k = 0; k < 4; ++k) zf[k] = st[L.zf + k * a.C + cc];
@@ -116,9 +150,9 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
     for (int k = 0; k < 5; ++k) acc[k] = st[L.acc + k * a.C + cc];
     const int64_t neq = a.cfg.neq, n = a.n;
     const double dt = a.cfg.dt;
-    for (int64_t tt = 0; tt < Tc; ++tt) {
+    // one sample of the stream (x = E at sample tt of this chunk)
+    auto sample = [&](double x, int64_t tt) {
         const int64_t t = t0 + tt;
-        const double x = (double)E[e_ld ? c * e_ld + tt : tt * a.C + c];
         // Balloon-Windkessel: BOLD[t] from the state after t steps (see oracle/wc_oracle.c orc_bold)
         const double iv = 1.0 / v;
         const double bold = a.vo * (a.k1 * (1.0 - q) + a.k2 * (1.0 - q * iv) + a.k3 * (1.0 - v));
@@ -138,12 +172,12 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
         f += dt * df;
         v += dt * dv;
         q += dt * dq;
-        if (t < neq) continue;
+        if (t < neq) return;
         const int64_t i = t - neq;  // data index of this BOLD sample
-        if (i >= n) continue;
+        if (i >= n) return;
         if (i >= n - 16) st[L.x16 + (i - (n - 16)) * a.C + c] = bold;
         if (i < 16) st[L.head + i * a.C + c] = bold;
-        if (i < kPad) continue;
+        if (i < kPad) return;
         if (i == kPad) {
             // odd extension in front: ext = 2 x0 - x[15..1], then x[0..15]; zi * ext[0]
             const double x0 = st[L.head + c];
@@ -169,7 +203,38 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
 #pragma unroll
             for (int k = 0; k < 4; ++k) st[L.zend + k * a.C + c] = zb[k];
         }
+    };
+    // samples are loaded 16 at a time ahead of their use; with COPY, each batch is
+    // loaded BEFORE the previous 32-sample tile's row stores are issued: vmcnt
+    // retires in issue order, so a load issued after those stores would wait for
+    // them (that ordering cost 7 ms per chunk at C3)
+    for (int64_t tb = 0; tb < Tc; tb += 16) {
+        float xr[16];
+        double xd[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int64_t tt = tb + j < Tc ? tb + j : tb;
+            const ET v = E[e_ld ? ce * e_ld + tt : tt * a.C + ce];
+            if constexpr (sizeof(ET) == 4) xr[j] = v; else xd[j] = v;
+        }
+        const int k0 = (int)(tb % kCopyT);
+        if constexpr (COPY) {
+            if (k0 == 0 && tb > 0) flush(tb - kCopyT, kCopyT);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (tb + j < Tc) {
+                const double x = sizeof(ET) == 4 ? (double)xr[j] : xd[j];
+                if constexpr (COPY) tile[lane * (kCopyT + 1) + k0 + j] = xr[j];
+                if (live) sample(x, tb + j);
+            }
+        }
     }
+    if constexpr (COPY) {
+        const int64_t last = ((Tc - 1) / kCopyT) * kCopyT;
+        flush(last, (int)(Tc - last));
+    }
+    if (!live) return;
     st[L.bal + c] = s;
     st[L.bal + a.C + c] = f;
     st[L.bal + 2 * a.C + c] = v;
@@ -744,7 +809,7 @@ int wc_bold_init(const wc_bold_cfg* cfg, int64_t C, double* state, void* stream)
 }
 
 int wc_bold_chunk(const wc_bold_cfg* cfg, int64_t C, const void* E, int e_f64, int64_t e_ld, int64_t t0,
-                  int64_t Tc, double* state, void* stream) {
+                  int64_t Tc, double* state, void* copy, int64_t copy_ld, void* stream) {
     wc_clear_err();
     int rc = check_cfg(cfg, C);
     if (rc) return rc;
@@ -754,12 +819,18 @@ int wc_bold_chunk(const wc_bold_cfg* cfg, int64_t C, const void* E, int e_f64, i
     const BoldArgs a = make_bold_args(cfg, C);
     hipStream_t st = static_cast<hipStream_t>(stream);
     const dim3 grid((unsigned)((C + 255) / 256));
+    if (copy && (e_f64 || e_ld != 0 || copy_ld < Tc))
+        return wc_set_err(WC_EINVAL, "wc_bold_chunk: copy needs fp32 time-major E and copy_ld >= Tc");
+    float* cp = static_cast<float*>(copy);
     if (e_f64)
-        hipLaunchKernelGGL(bold_chunk_kernel<double>, grid, dim3(256), 0, st, a, static_cast<const double*>(E), e_ld,
-                           t0, Tc, state);
+        hipLaunchKernelGGL((bold_chunk_kernel<double, false>), grid, dim3(256), 0, st, a,
+                           static_cast<const double*>(E), e_ld, t0, Tc, state, cp, copy_ld);
+    else if (copy)
+        hipLaunchKernelGGL((bold_chunk_kernel<float, true>), grid, dim3(256), 0, st, a, static_cast<const float*>(E),
+                           e_ld, t0, Tc, state, cp, copy_ld);
     else
-        hipLaunchKernelGGL(bold_chunk_kernel<float>, grid, dim3(256), 0, st, a, static_cast<const float*>(E), e_ld, t0,
-                           Tc, state);
+        hipLaunchKernelGGL((bold_chunk_kernel<float, false>), grid, dim3(256), 0, st, a, static_cast<const float*>(E),
+                           e_ld, t0, Tc, state, cp, copy_ld);
     return wc_hip_check("wc_bold_chunk");
 }
 

@@ -12,10 +12,11 @@ do one simulation at a time:
   utils.kuramoto(BOLD), np.mean(sFC)                                  -> wc_hilbert_phase + wc_fc_metrics
 
 The recorded phase runs in chunks of `chunk_samples` samples (20 Euler steps
-each).  Each chunk's E samples land node-major in one slot of a 4-slot ring
-([C][4*chunk] fp32, 28.8 GB at 20,000 x 90); the BOLD stream consumes the slot
-right away and every completed 4000-sample Welch segment is transformed from
-the ring -- the 648 MB/simulation trajectory of the reference never exists.
+each).  The integrator writes each chunk time-major ([chunk][C] fp32, 7.2 GB
+at 20,000 x 90: full-line stores); the BOLD stream consumes it right away and
+in the same pass writes it node-major into one slot of a 4-slot ring ([C][4*chunk]
+fp32, 28.8 GB), from which every completed 4000-sample Welch segment is
+transformed -- the 648 MB/simulation trajectory of the reference never exists.
 """
 from __future__ import annotations
 
@@ -86,14 +87,21 @@ def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedul
     nslots = WELCH_NPERSEG // chunk_samples
     ld = nslots * chunk_samples
     ring = torch.empty(C * ld, dtype=bt.rec_dtype, device=bt.device)
+    # fp32: the integrator writes each chunk time-major (full-line stores) and the BOLD
+    # pass transposes it into the node-major Welch ring; fp64: straight into the ring
+    tmaj = torch.empty(chunk_samples * C, dtype=bt.rec_dtype, device=bt.device) if precision == F32 else None
     bold = BoldStream(C, T, NEQ, bold_downsamp, p.dt * p.downsamp, bt.device)  # BOLD_dt = dt*downsamp (wc:144)
     welch = WelchAccumulator(B, N, bt.device) if T >= WELCH_NPERSEG else None
     next_seg, t_done, k = 0, 0, 0
     while t_done < T:
         n_samp = min(chunk_samples, T - t_done)
         slot = k % nslots
-        bt.integrate(n_samp * R, sch.tau_ip[2], R, ring[slot * chunk_samples:], rec_ld=ld)
-        bold.feed(ring, n_samp, e_ld=ld, offset=slot * chunk_samples)
+        if tmaj is not None:
+            bt.integrate(n_samp * R, sch.tau_ip[2], R, tmaj)
+            bold.feed(tmaj, n_samp, e_ld=0, copy=ring, copy_ld=ld, copy_offset=slot * chunk_samples)
+        else:
+            bt.integrate(n_samp * R, sch.tau_ip[2], R, ring[slot * chunk_samples:], rec_ld=ld)
+            bold.feed(ring, n_samp, e_ld=ld, offset=slot * chunk_samples)
         t_done += n_samp
         k += 1
         while welch is not None and next_seg * WELCH_HOP + WELCH_NPERSEG <= t_done:

@@ -51,16 +51,19 @@ class BoldStream:
                    "wc_bold_init")
         self.t = 0
 
-    def feed(self, E, Tc=None, e_ld=0, offset=0):
+    def feed(self, E, Tc=None, e_ld=0, offset=0, copy=None, copy_ld=0, copy_offset=0):
         """Feed the next Tc samples.  E time-major [Tc][C] (e_ld=0), or a node-major
-        buffer with sample tt of column c at flat index offset + c*e_ld + tt."""
+        buffer with sample tt of column c at flat index offset + c*e_ld + tt.
+        copy (fp32 time-major E only): also write the chunk node-major into
+        copy at flat index copy_offset + c*copy_ld + tt (the Welch ring)."""
         if Tc is None:
             Tc = E.shape[0]
         f64 = E.dtype == torch.float64
         if not f64 and E.dtype != torch.float32:
             raise TypeError("E must be float32 or float64")
+        cp = _ptr_at(copy, copy_offset) if copy is not None else None
         rc = _lib.lib().wc_bold_chunk(ctypes.byref(self.cfg), self.C, _ptr_at(E, offset), int(f64), e_ld, self.t,
-                                      Tc, _lib.ptr(self.state), _lib.stream_handle())
+                                      Tc, _lib.ptr(self.state), cp, copy_ld, _lib.stream_handle())
         _lib.check(rc, "wc_bold_chunk")
         self.t += Tc
 

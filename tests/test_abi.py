@@ -30,7 +30,7 @@ def test_library_exports_header_symbols():
 def test_abi_version_and_workspace():
     from nremmodfc_amd import _lib
     L = _lib.lib()
-    assert L.wcsde_abi_version() == 2
+    assert L.wcsde_abi_version() == 3
     assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16   # bf16x6 image
     assert L.wc_workspace_size(20000, 90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
     assert L.wc_workspace_size(1, 16, _lib.WC_F32) == 2 * 1 * 3 * 64 * 16

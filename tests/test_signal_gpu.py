@@ -57,6 +57,37 @@ def test_bold_chunking_is_exact(cuda):
     assert torch.equal(one, bs2.finish())
 
 
+@pytest.mark.parametrize("C", [5, 300, 700])
+def test_bold_copy_transposes_into_ring(cuda, C):
+    """wc_bold_chunk's copy output: the fp32 time-major chunk lands node-major in
+    the ring slot (ragged chunk lengths and column counts), and the BOLD result is
+    unchanged."""
+    T = 6_000
+    E = torch.from_numpy(_e_like(T, C, C)).float().cuda()
+    ref = wsg.BoldStream(C, T, dec=1000)
+    ref.feed(E)
+    want = ref.finish()
+    ld = 4000
+    ring = torch.full((C * ld,), float("nan"), dtype=torch.float32, device="cuda")
+    bs = wsg.BoldStream(C, T, dec=1000)
+    t = 0
+    for n in (1000, 37, 963, 1000, 1000, 1000, 1000, 1000 - 0):
+        n = min(n, T - t)
+        if n <= 0:
+            break
+        slot_off = (t % ld)
+        if slot_off + n > ld:  # keep each chunk inside the ring (test layout only)
+            n = ld - slot_off
+        bs.feed(E[t:t + n].contiguous(), copy=ring, copy_ld=ld, copy_offset=slot_off)
+        got = ring.view(C, ld)[:, slot_off:slot_off + n]
+        assert torch.equal(got, E[t:t + n].t()), (t, n)
+        t += n
+    while t < T:  # the rest without copies
+        bs.feed(E[t:T].contiguous())
+        t = T
+    assert torch.equal(bs.finish(), want)
+
+
 def test_fc_metrics_vs_oracle(cuda):
     rng = np.random.default_rng(3)
     B, N, M = 5, 90, 298
