@@ -68,18 +68,33 @@ __device__ __forceinline__ void philox_ctr(uint64_t step, uint32_t quad, uint64_
 __device__ __forceinline__ float u01f(uint32_t x) { return (float)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8f; }
 __device__ __forceinline__ double u01d(uint32_t x) { return (double)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8; }
 
-// fp32: hardware transcendentals.  ln u = log2(u) ln2; v_sin/v_cos take
-// revolutions (sin(2 pi x)).  Inputs are never denormal: u >= 2^-24.
-__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, float z[4]) {
+// the same u as u01f in two VALU ops: (1 + m 2^-23) - (1 - 2^-24) = (2m + 1) 2^-24
+// exactly (Sterbenz; the result is an odd multiple of 2^-24 below 1: 24 bits)
+__device__ __forceinline__ float u01f_fast(uint32_t x) {
+    return __uint_as_float((x >> 9) | 0x3F800000u) - 0.99999994039535522461f;
+}
+
+// fp32, unscaled: z / sqrt(2 ln 2) = sqrt(-log2 u0) (cos, sin)(2 pi u1) -- the caller
+// folds sqrt(2 ln 2) into its noise scale.  Hardware transcendentals; v_sin/v_cos
+// take revolutions; inputs are never denormal (u >= 2^-24).
+constexpr float kSqrt2Ln2 = 1.1774100225154747f;
+__device__ __forceinline__ void quad_normals_raw(uint64_t step, uint32_t q, uint64_t key, float z[4]) {
     uint32_t x[4];
     philox_ctr(step, q, key, x);
-    const float r0 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[0])));
-    const float r1 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u01f(x[2])));
-    const float a0 = u01f(x[1]), a1 = u01f(x[3]);
+    const float r0 = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u01f_fast(x[0])));
+    const float r1 = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u01f_fast(x[2])));
+    const float a0 = u01f_fast(x[1]), a1 = u01f_fast(x[3]);
     z[0] = r0 * __builtin_amdgcn_cosf(a0);
     z[1] = r0 * __builtin_amdgcn_sinf(a0);
     z[2] = r1 * __builtin_amdgcn_cosf(a1);
     z[3] = r1 * __builtin_amdgcn_sinf(a1);
+}
+
+// fp32 standard normals (test hook, N > 96 path)
+__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, float z[4]) {
+    quad_normals_raw(step, q, key, z);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[i] *= kSqrt2Ln2;
 }
 
 // fp64: correctly rounded-ish libm (ocml); sincospi reduces 2u exactly
@@ -155,6 +170,8 @@ template <> struct AccA<true> {
     __device__ void set(double x) { hi = (float)x; lo = (float)(x - (double)hi); }
     __device__ double get() const { return (double)hi + (double)lo; }
     template <typename Real> __device__ Real val() const { return (Real)(hi + lo); }
+    // fp32 value: |lo| <= ulp(hi)/2 after every add, so round(hi + lo) == hi (up to ties)
+    __device__ float fast() const { return hi; }
     __device__ void add(float inc) {  // Kahan-Babuska: |hi| >> |inc|
         const float t = inc + lo;
         const float s = hi + t;

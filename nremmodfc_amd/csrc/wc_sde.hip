@@ -140,6 +140,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr bool kMfma = (VAR & V_NO_MFMA) == 0;
     constexpr bool kPairA = sizeof(Real) == 4 && (VAR & V_KAHAN_A) != 0;
     constexpr bool kParamRegs = sizeof(Real) == 4;  // fp64 re-reads G/sigmaE (register budget)
+    // fp32 with the compensated a_ie: the folded-constant update (Sl holds -sigmaE log2 e)
+    constexpr bool kFast = sizeof(Real) == 4 && kPairA;
     constexpr int kFragUnits = kBf ? NT * NC * 3 : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -205,7 +207,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             A[u][r].set(ok ? a.A[o] : 0.0);
             if constexpr (kParamRegs) {
                 Gc[u][r] = ok ? (Real)a.G[o] : (Real)0;
-                Sl[u][r] = ok ? Tr<Real>::slope(a.sigmaE[o]) : (Real)0;
+                Sl[u][r] = ok ? (kFast ? -1 : 1) * Tr<Real>::slope(a.sigmaE[o]) : (Real)0;
             }
         }
 
@@ -258,6 +260,11 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     const Real a_ee = (Real)a.a_ee, a_ei = (Real)a.a_ei, a_ii = (Real)a.a_ii;
     const Real P = (Real)a.P, rhoE = (Real)a.rhoE, rE = (Real)a.rE, rI = (Real)a.rI;
     const Real mu = (Real)a.mu, slI = Tr<Real>::slope(a.sigmaI), sqdtD = (Real)a.sqdtD;
+    // fp32 product path: folded constants (see the kFast update)
+    const float Pm = (float)(a.P - a.mu), knoise = (float)(a.sqdtD * (double)kSqrt2Ln2);
+    const float cIe = (float)(-a.a_ei * a.sigmaI * 1.4426950408889634);
+    const float cIi = (float)(a.a_ii * a.sigmaI * 1.4426950408889634);
+    const float cI0 = (float)(a.mu * a.sigmaI * 1.4426950408889634);
     const Real dtE = (Real)(a.dtSim / a.tauE), dtI = (Real)(a.dtSim / a.tauI);
     const Real dt = (Real)a.dtSim;
     const Real dtA = (Real)(a.dtSim / a.tau_ip);
@@ -394,6 +401,30 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         for (int u = 0; u < OT; ++u) {
             if constexpr (sizeof(Real) == 8) __builtin_amdgcn_sched_barrier(0);  // fp64: bound live ranges
             Real z[4] = {0, 0, 0, 0};
+            if constexpr (kFast) {
+                if constexpr (kRng) quad_normals_raw(gstep, (uint32_t)(4 * (T0 + u) + g), key, z);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    // wc:80-83 in fp32 with the constants folded:
+                    //   x' = xE - mu; SE = 1/(1 + 2^(x' * (-sigmaE log2 e)));
+                    //   SI = 1/(1 + 2^(e cIe + in cIi + cI0)); noise = knoise * raw normal
+                    const float e = E[u][r], in = I[u][r];
+                    const float ai = A[u][r].fast();
+                    const float cpl = kMfma ? acc[u][r] : e;
+                    float x = __builtin_fmaf(a_ee, e, Pm);
+                    x = __builtin_fmaf(-ai, in, x);
+                    x = __builtin_fmaf(Gc[u][r], cpl, x);
+                    x = __builtin_fmaf(knoise, z[r], x);
+                    const float SE = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * Sl[u][r]));
+                    const float SI = __builtin_amdgcn_rcpf(
+                        1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(e, cIe, __builtin_fmaf(in, cIi, cI0))));
+                    E[u][r] = __builtin_fmaf(dtE, __builtin_fmaf(__builtin_fmaf(-rE, e, 1.0f), SE, -e), e);
+                    I[u][r] = __builtin_fmaf(dtI, __builtin_fmaf(__builtin_fmaf(-rI, in, 1.0f), SI, -in), in);
+                    const float tA = in * dtA;
+                    A[u][r].add(__builtin_fmaf(e, tA, -rhoE * tA));
+                }
+                continue;
+            }
             if constexpr (kRng) quad_normals(gstep, (uint32_t)(4 * (T0 + u) + g), key, z);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
