@@ -200,3 +200,17 @@ def test_grouped_kernel_ring_records(cuda, sc90, nsteps):
     assert torch.equal(nm, tm)
     assert torch.isnan(ring.view(B * 90, ld)[:, 4 + n_rec:]).all()  # nothing written past the last record
     assert torch.equal(a.E, b.E)
+
+
+@pytest.mark.parametrize("N,B", [(7, 1), (16, 5), (20, 17), (33, 40), (64, 3), (81, 2), (96, 33)])
+def test_f32_shapes_and_tails(cuda, N, B):
+    """Every fp32 tile configuration (NT = 2, 4, 6) with ragged N and B vs the oracle."""
+    rng = np.random.default_rng(N + 1000)
+    sc = rng.uniform(size=(N, N)) * (rng.uniform(size=(N, N)) < 0.5)
+    sc = (sc + sc.T) / 2
+    np.fill_diagonal(sc, 0)
+    sc *= 2.51 / max(sc.sum(1).mean(), 1e-12)
+    keys = sim_keys(list(range(B)), [N] * B)
+    g, o, *_ = run_pair(sc, 0.16, 7.68, keys, 100, 0, 200, 20, "f32")
+    d = np.abs(g - o)
+    assert d.max() <= 2e-3 and np.sqrt(np.mean(d ** 2)) <= 2e-4, (d.max(), np.sqrt(np.mean(d ** 2)))

@@ -144,3 +144,21 @@ def test_sweep_main_short(tmp_path, cuda):
     assert (df["corrW"].abs() <= 1).all() and (df["peakfreq"] > 0).all()
     sweep.main(["homo", "--seeds", "1", "--short", "--limit", "6", "--out", out, "--tag", "t"])
     assert len(pd.read_csv(os.path.join(out, "t.txt"))) == 6
+
+
+@pytest.mark.gpu
+def test_many_seeds_main_short(tmp_path, cuda):
+    """run_many_seeds.py drop-in: (seed, state) keys, the reference's HMA dict per
+    simulation and the "metainfo" counts (run_many_seeds.py:130-146)."""
+    import pickle
+    out = str(tmp_path)
+    sweep.main(["many", "--modality", "homo", "--seeds", "2", "--short", "--out", out, "--tag", "m"])
+    with open(os.path.join(out, "m.pickle"), "rb") as f:  # our own file
+        d = pickle.load(f)
+    assert d["metainfo"] == {s: 2 for s in datasets.STATES}
+    keys = [k for k in d if k != "metainfo"]
+    assert sorted(keys) == sorted(itertools.product(range(2), datasets.STATES))
+    v = d[(0, "W")]
+    assert set(v) == {"Hin_sim", "Hse_sim", "Hin_node_sim", "Hse_node_sim", "sFC"}
+    assert v["sFC"].shape == (90, 90) and (v["sFC"] >= 0).all()  # clipped in place like the reference
+    assert v["Hin_node_sim"].shape == (90,) and np.isfinite(v["Hin_sim"])
