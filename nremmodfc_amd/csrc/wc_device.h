@@ -143,14 +143,22 @@ template <> struct Tr<double> {
 
 // v = hi + mid + lo, each a bf16: |v - hi - mid - lo| <= 2^-27 |v|
 __device__ __forceinline__ void split3(const float v[4], bf16x4& hi, bf16x4& mid, bf16x4& lo) {
+    // pairwise: one v_cvt_pk_bf16_f32 (RNE) per two values and part, residuals by packed subtracts
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const __bf16 h = (__bf16)v[i];
-        const float r = v[i] - (float)h;
-        const __bf16 m = (__bf16)r;
-        hi[i] = h;
-        mid[i] = m;
-        lo[i] = (__bf16)(r - (float)m);
+    for (int p = 0; p < 2; ++p) {
+        const f2 x = {v[2 * p], v[2 * p + 1]};
+        const b2 h = __builtin_convertvector(x, b2);
+        const f2 r = x - __builtin_convertvector(h, f2);
+        const b2 m = __builtin_convertvector(r, b2);
+        const b2 l = __builtin_convertvector(r - __builtin_convertvector(m, f2), b2);
+        hi[2 * p] = h[0];
+        hi[2 * p + 1] = h[1];
+        mid[2 * p] = m[0];
+        mid[2 * p + 1] = m[1];
+        lo[2 * p] = l[0];
+        lo[2 * p + 1] = l[1];
     }
 }
 

@@ -154,19 +154,33 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
     auto sample = [&](double x, int64_t tt) {
         const int64_t t = t0 + tt;
         // Balloon-Windkessel: BOLD[t] from the state after t steps (see oracle/wc_oracle.c orc_bold)
-        const double iv = 1.0 / v;
-        const double bold = a.vo * (a.k1 * (1.0 - q) + a.k2 * (1.0 - q * iv) + a.k3 * (1.0 - v));
-        double vpow;
+        double iv, vpow, vpow_iv;
         if (a.alpha_3125) {
-            const double r8 = sqrt(sqrt(sqrt(v)));
-            vpow = v * v * v * r8;
+            // z = v^(-1/8): fp32 seed, two division-free Newton steps z <- z (1 + (1 - v z^8)/8)
+            // (relative error ~1e-16); then 1/v = z^8 and v^(1/alpha) = v^3.125 = v^4 z^7
+            double z = (double)__builtin_amdgcn_rsqf(__builtin_sqrtf(__builtin_sqrtf((float)v)));
+#pragma unroll
+            for (int it = 0; it < 2; ++it) {
+                const double z2 = z * z, z4 = z2 * z2;
+                z = fma(z * 0.125, fma(-v, z4 * z4, 1.0), z);
+            }
+            const double z2 = z * z, z4 = z2 * z2, z7 = z4 * z2 * z, v2 = v * v;
+            iv = z4 * z4;
+            vpow = v2 * v2 * z7;      // v^3.125
+            vpow_iv = v2 * v * z7;    // v^2.125 = vpow / v
         } else {
+            iv = 1.0 / v;
             vpow = exp(log(v) * a.ialpha);
+            vpow_iv = vpow * iv;
         }
-        const double fpow = exp(a.log1mEo / f);
+        const double bold = a.vo * (a.k1 * (1.0 - q) + a.k2 * (1.0 - q * iv) + a.k3 * (1.0 - v));
+        double rf = (double)__builtin_amdgcn_rcpf((float)f);  // 1/f: fp32 seed + two Newton steps
+        rf = fma(rf, fma(-f, rf, 1.0), rf);
+        rf = fma(rf, fma(-f, rf, 1.0), rf);
+        const double fpow = exp(a.log1mEo * rf);
         const double ds = x - a.itaus * s - a.itauf * (f - 1.0);
         const double dv = (f - vpow) * a.itauo;
-        const double dq = (f * (1.0 - fpow) * a.iEo - q * vpow * iv) * a.itauo;
+        const double dq = (f * (1.0 - fpow) * a.iEo - q * vpow_iv) * a.itauo;
         const double df = s;
         s += dt * ds;
         f += dt * df;

@@ -49,6 +49,12 @@ __global__ void twiddle_kernel(double* tw) {
     tw[2 * m + 1] = -s;
     float2* tw32 = reinterpret_cast<float2*>(tw + 2 * kSeg);
     tw32[m] = make_float2((float)c, (float)-s);
+    // periodic Hann pairs for the packed samples (2j, 2j+1): hann2[j] = (w(2j), w(2j+1))
+    if ((m & 1) == 0) {
+        double s1, c1;
+        sincospi(2.0 * (m + 1) / kSeg, &s1, &c1);
+        reinterpret_cast<float2*>(tw32 + kSeg)[m >> 1] = make_float2((float)(0.5 - 0.5 * c), (float)(0.5 - 0.5 * c1));
+    }
 }
 
 template <typename R>
@@ -277,9 +283,9 @@ __device__ __forceinline__ void wstage(float2* z, const float2* __restrict__ tw,
             if (i < S) {
 #pragma unroll
                 for (int r = 0; r < RAD; ++r) {
-                    const int m = i + r * S;  // samples 2m, 2m+1
-                    u[q][r].x = (u[q][r].x - mean) * (0.5f - 0.5f * tw[2 * m].x);
-                    u[q][r].y = (u[q][r].y - mean) * (0.5f - 0.5f * tw[2 * m + 1].x);
+                    const float2 w = tw[kSeg + i + r * S];  // (w(2m), w(2m+1)) of the Hann table after the twiddles
+                    u[q][r].x = (u[q][r].x - mean) * w.x;
+                    u[q][r].y = (u[q][r].y - mean) * w.y;
                 }
             }
         }
@@ -291,8 +297,10 @@ __device__ __forceinline__ void wstage(float2* z, const float2* __restrict__ tw,
         const int i = lane + 64 * q;
         if (i < S) {
             const int k = i % P;
+            if constexpr (P > 1) {  // first stage: every twiddle is 1
 #pragma unroll
-            for (int r = 1; r < RAD; ++r) u[q][r] = cmulf(u[q][r], tw[r * k * TS]);
+                for (int r = 1; r < RAD; ++r) u[q][r] = cmulf(u[q][r], tw[r * k * TS]);
+            }
             float2 U[RAD];
             if constexpr (RAD == 4) {
                 const float2 a = make_float2(u[q][0].x + u[q][2].x, u[q][0].y + u[q][2].y);
@@ -454,7 +462,9 @@ __global__ void welch_peak_kernel(int B, int N, int nseg, double fs, const doubl
 
 extern "C" {
 
-size_t wc_welch_workspace_size(void) { return (size_t)kSeg * 2 * sizeof(double) + (size_t)kSeg * sizeof(float2); }
+size_t wc_welch_workspace_size(void) {
+    return (size_t)kSeg * 2 * sizeof(double) + (size_t)kSeg * sizeof(float2) + (size_t)kFFT * sizeof(float2);
+}
 int wc_welch_bins(void) { return kBins; }
 
 int wc_welch_prepare(void* workspace, size_t ws_bytes, void* stream) {
