@@ -69,7 +69,7 @@ const char* wc_last_error(void);
 /* Bytes of device workspace wc_integrate needs for B simulations of an N-node
  * connectome.  N <= 96: the connectome's MFMA A-operand image only (state stays
  * in registers for the whole call).  N > 96: the A-operand image plus the
- * tile-major state image and the double-buffered E operand (28 B per
+ * tile-major state image and the double-buffered E operand (32 B per
  * node-simulation in fp32, padded to multiples of 64 nodes and simulations). */
 size_t wc_workspace_size(int B, int N, int precision);
 

@@ -7,14 +7,16 @@
 // launch of a GEMM-shaped kernel whose epilogue is the elementwise update:
 //
 //   * workgroup tile = 64 nodes x 64 simulations, 4 waves of 32 x 32
-//     (2 x 2 MFMA 16x16 tiles); K loop over 32-node chunks;
+//     (2 x 2 MFMA 16x16 tiles); K loop over 32-node chunks fed by LDS-DMA
+//     (global_load_lds_dwordx4) into 2 LDS stages (48 KB, 3 workgroups per CU;
+//     3 stages at 2 workgroups per CU measured slower, as did prefetching the
+//     epilogue state into registers: tools/diag_large.py variants 104, 105);
 //   * fp32 product path: CM and E as three bf16 parts each, six cross terms on
 //     v_mfma_f32_16x16x32_bf16 (fp32-equivalent, as in wc_sde.hip).  CM's
-//     parts are pre-split in the A-operand image; E is kept as ONE fp32 image
-//     in B-operand order (the epilogue writes it in place) and split exactly
-//     (hi + mid + lo == v for any fp32 v) while a chunk is staged into LDS:
-//     each workgroup fetches every A/E chunk once into a double-buffered LDS
-//     stage and its waves read their fragments with ds_read_b128;
+//     parts are pre-split in the A-operand image; E is kept ONLY as its exact
+//     3-way split (hi + mid + lo == E for fp32 E), written by the epilogue in
+//     the lane-linear order the DMA needs (xs_index), so the K loop is DMA +
+//     ds_read_b128 + MFMA with no VALU;
 //   * fp64 parity path: v_mfma_f64_16x16x4_f64 on fp64 E;
 //   * the MFMA D fragment of a lane is 4 consecutive nodes of one simulation
 //     = exactly one Philox4x32-10 call (quad = node/4): the epilogue draws the
@@ -32,6 +34,7 @@
 
 namespace {
 using namespace wcdev;
+typedef __attribute__((address_space(3))) void* lds_vptr;
 
 constexpr int kTile = 64;  // node and simulation padding unit (workgroup tile edge)
 
@@ -62,8 +65,8 @@ Geo geometry(int B, int N, int precision) {
         g.o_Alo = o; o += al(cells * 4);
         g.o_G = o; o += al(cells * 4);
         g.o_S = o; o += al(cells * 4);
-        g.o_X0 = o; o += al(cells * 4);  // fp32 E, split to bf16 parts while staged into LDS
-        g.o_X1 = o; o += al(cells * 4);
+        g.o_X0 = o; o += al(cells * 6);  // E as three bf16 parts in LDS-DMA order (xs_index)
+        g.o_X1 = o; o += al(cells * 6);
     } else {
         o += al((size_t)g.MT * g.KC4 * 64 * 8);
         g.o_E = 0;
@@ -97,12 +100,16 @@ __host__ __device__ __forceinline__ size_t tm_index(const Geo& g, int b, int n) 
     return ((((size_t)(b >> 4) * g.MT + (n >> 4)) * 64 + lane) << 2) + (n & 3);
 }
 
-// fp32 B-operand image of E: node n, sim b at [c = n/32][b][g = (n%16)/4][h = (n/16)%2][r = n%4]:
-// the 8 floats of (c, b, g) are, in order, lane (g, b%16)'s B operand of k-chunk c
-// (matches the A image: k element jj = 4h + r <-> node 16(2c + h) + 4g + r)
-__host__ __device__ __forceinline__ size_t x32_index(const Geo& g, int b, int n) {
+// bf16 B-operand image of E (three parts, exact: hi + mid + lo == E for fp32 E):
+// 16-B unit ((p*NC + c)*SB + b/64)*256 + g*64 + b%64 holds, for part p, k-chunk
+// c = n/32, node group g = (n%16)/4 and simulation b, the 8 values jj = 4h + r of
+// nodes 16(2c + h) + 4g + r -- lane (g, b%16)'s operand.  A workgroup's (p, c)
+// slab of 64 simulations is 4 KB contiguous and lands lane-linear in LDS by
+// global_load_lds (position g*64 + b%64), where the wave reads it back.
+__host__ __device__ __forceinline__ size_t xs_index(const Geo& g, int p, int b, int n) {
     const int c = n >> 5, h = (n >> 4) & 1, gg = (n & 15) >> 2, r = n & 3;
-    return (((size_t)c * g.Bp + b) * 4 + gg) * 8 + 4 * h + r;
+    const size_t unit = (((size_t)p * g.NC + c) * (g.Bp / kTile) + (b >> 6)) * 256 + gg * 64 + (b & 63);
+    return unit * 8 + 4 * h + r;
 }
 
 // f64 B operand: E of node n = 4c + k, sim b at [c][b][k]
@@ -159,7 +166,15 @@ __global__ void prep_kernel(LArgs a, const double* __restrict__ G, const double*
     const double gc = ok ? G[o] : 0.0, s = ok ? sigmaE[o] : 0.0;
     const size_t t = tm_index(g, b, n);
     if constexpr (sizeof(Real) == 4) {
-        reinterpret_cast<float*>(a.ws + g.o_X0)[x32_index(g, b, n)] = (float)e;
+        {
+            float v[4] = {(float)e, 0.f, 0.f, 0.f};
+            bf16x4 h, m, l;
+            split3(v, h, m, l);
+            __bf16* X = reinterpret_cast<__bf16*>(a.ws + g.o_X0);
+            X[xs_index(g, 0, b, n)] = h[0];
+            X[xs_index(g, 1, b, n)] = m[0];
+            X[xs_index(g, 2, b, n)] = l[0];
+        }
         reinterpret_cast<float*>(a.ws + g.o_I)[t] = (float)in;
         AccA<true> acc;
         acc.set(ai);
@@ -185,7 +200,8 @@ __global__ void finish_kernel(LArgs a, int buf, double* __restrict__ E, double* 
     const int b = (int)(idx / g.N), n = (int)(idx % g.N);
     const size_t t = tm_index(g, b, n);
     if constexpr (sizeof(Real) == 4) {
-        E[idx] = reinterpret_cast<const float*>(a.ws + (buf ? g.o_X1 : g.o_X0))[x32_index(g, b, n)];
+        const __bf16* X = reinterpret_cast<const __bf16*>(a.ws + (buf ? g.o_X1 : g.o_X0));
+        E[idx] = ((float)X[xs_index(g, 0, b, n)] + (float)X[xs_index(g, 1, b, n)]) + (float)X[xs_index(g, 2, b, n)];
         I[idx] = reinterpret_cast<const float*>(a.ws + g.o_I)[t];
         A[idx] = (double)reinterpret_cast<const float*>(a.ws + g.o_Ahi)[t] +
                  (double)reinterpret_cast<const float*>(a.ws + g.o_Alo)[t];
@@ -214,7 +230,7 @@ __device__ __forceinline__ void tile_of(const Geo& g, int& sb, int& mb) {
 // one Euler step of every simulation; rec_row >= 0: record the state before the update
 // DIAG (ablation, tools/diag_large.py): 1 = no chunk fetch (LDS reused),
 // 2 = no MFMA, 3 = no epilogue state traffic (noise + math only), 0 = product
-template <typename Real, int DIAG = 0>
+template <typename Real, int DIAG = 0, int STAGES = 2, bool PF = false>
 __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec_row, int buf) {
     typedef typename Tr<Real>::acc_t acc_t;
     typedef __attribute__((ext_vector_type(4))) Real real4;
@@ -234,60 +250,79 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
 #pragma unroll
         for (int v = 0; v < NV; ++v) acc[u][v] = acc_t{0, 0, 0, 0};
 
+    // PF (fp32): the epilogue's I and a_ie pair are loaded before the K loop, so their
+    // latency hides behind it (48 VGPRs); G and sigmaE are read at the epilogue
+    constexpr bool kPF = PF && sizeof(Real) == 4;
+    real4 pfI[kPF ? NV : 1][kPF ? NU : 1], pfH[kPF ? NV : 1][kPF ? NU : 1], pfL[kPF ? NV : 1][kPF ? NU : 1];
+    if constexpr (kPF) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const size_t t4 = ((size_t)(s0 + v) * g.MT + m0 + u) * 64 + lane;
+                pfI[v][u] = reinterpret_cast<const real4*>(a.ws + g.o_I)[t4];
+                pfH[v][u] = reinterpret_cast<const real4*>(a.ws + g.o_Ahi)[t4];
+                pfL[v][u] = reinterpret_cast<const real4*>(a.ws + g.o_Alo)[t4];
+            }
+    }
+
     if constexpr (sizeof(Real) == 4) {
-        // Each 32-node k-chunk of the workgroup's A rows (4 tiles x 3 parts) and
-        // E columns (4 sim tiles x 3 parts) is fetched ONCE per workgroup into a
-        // double-buffered LDS stage (2 x 24 KB; 6 x 16 B per thread, 1-3 KB
-        // contiguous runs), then every wave reads its fragments with
-        // ds_read_b128.  The fetch of chunk c+1 is in flight during chunk c's 96 MFMAs.
-        __shared__ bf16x8 lds[2][2][4 * 3 * 64];  // [stage][A|B][tile*3 + part][lane]
+        // K loop fed by LDS-DMA: each 32-node k-chunk of the workgroup's A rows
+        // (4 tiles x 3 parts, pre-split image) and E columns (3 parts x 64 sims,
+        // pre-split by the previous step's epilogue) is 24 x 1 KB lane-linear
+        // global_load_lds_dwordx4 into a ring of STAGES LDS stages (6 per wave),
+        // STAGES-1 chunks in flight; a counted vmcnt + raw s_barrier retire a stage.
+        // The loop body is then only ds_read_b128 + MFMA (no VALU staging).
+        __shared__ bf16x8 lds[STAGES][2][12 * 64];  // [stage][A | B][unit][lane]
         const bf16x8* F = reinterpret_cast<const bf16x8*>(a.ws + g.o_frag);
-        const f32x4* X = reinterpret_cast<const f32x4*>(a.ws + (buf ? g.o_X1 : g.o_X0));
-        const int t = threadIdx.x;
-        // A: unit q = t + 256 i (i = 0..2) of the 768-unit pre-split slab: tile = q / 192, rem = q % 192
-        const bf16x8* fsrc[3];
+        const bf16x8* X = reinterpret_cast<const bf16x8*>(a.ws + (buf ? g.o_X1 : g.o_X0));
+        const int SB = g.Bp / kTile;
+        // this wave's 3 A units (tile ta, part pa) and 3 B units (part pb, group gb)
+        const bf16x8* asrc[3];
+        const bf16x8* bsrc[3];
+        int aoff[3], boff[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const int q = t + 256 * i;
-            fsrc[i] = F + (size_t)(mb * 4 + q / 192) * g.NC * 192 + q % 192;
+            const int ua = 3 * w + i, ta = ua / 3, pa = ua % 3;
+            asrc[i] = F + ((size_t)(mb * 4 + ta) * g.NC * 3 + pa) * 64 + lane;  // + c * 192
+            aoff[i] = (ta * 3 + pa) * 64;
+            const int ub = 3 * w + i, pb = ub / 4, gb = ub % 4;
+            bsrc[i] = X + (((size_t)pb * g.NC * SB + sb) * 256 + gb * 64) + lane;  // + c * SB * 256
+            boff[i] = (pb * 4 + gb) * 64;
         }
-        // B: thread t = 4 * sim + g loads the 8 fp32 E of (chunk, sim, g) and splits them
-        const int bsim = t >> 2, bg = t & 3;
-        const f32x4* xsrc = X + ((size_t)(sb * 64 + bsim) * 4 + bg) * 2;
-        const int bdst = ((bsim >> 4) * 3) * 64 + 16 * bg + (bsim & 15);  // [tile][part 0][lane]
-        const size_t xstep = (size_t)g.Bp * 4 * 2;
-        // register ring of two in-flight chunks: chunk c+2 is fetched while chunk c
-        // is on the MFMA and chunk c+1 (fetched one iteration earlier) is being stashed
-        bf16x8 ra[2][3];
-        f32x4 rb[2][2];
-        auto fetch = [&](int c, int q) {
+        const size_t bstep = (size_t)SB * 256;
+        auto issue = [&](int c, int st) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) ra[q][i] = fsrc[i][(size_t)c * 192];
-            rb[q][0] = xsrc[(size_t)c * xstep];
-            rb[q][1] = xsrc[(size_t)c * xstep + 1];
-        };
-        auto stash = [&](int st, int q) {
-#pragma unroll
-            for (int i = 0; i < 3; ++i) lds[st][0][t + 256 * i] = ra[q][i];
-            bf16x4 h0, m0, l0, h1, m1, l1;
-            const float v0[4] = {rb[q][0][0], rb[q][0][1], rb[q][0][2], rb[q][0][3]};
-            const float v1[4] = {rb[q][1][0], rb[q][1][1], rb[q][1][2], rb[q][1][3]};
-            split3(v0, h0, m0, l0);
-            split3(v1, h1, m1, l1);
-            lds[st][1][bdst] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-            lds[st][1][bdst + 64] = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
-            lds[st][1][bdst + 128] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+            for (int i = 0; i < 3; ++i) {
+                __builtin_amdgcn_global_load_lds(asrc[i] + (size_t)c * 192, (lds_vptr)(&lds[st][0][aoff[i]]), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(bsrc[i] + (size_t)c * bstep, (lds_vptr)(&lds[st][1][boff[i]]), 16, 0, 0);
+            }
         };
         const int ua = (w & 1) * 2, ub = (w >> 1) * 2;  // this wave's tiles within the workgroup slab
-        auto body = [&](int c, int q) {  // q = c & 1 (compile-time at each call site)
-            if (DIAG != 1 && c + 2 < g.NC) fetch(c + 2, q);
+#pragma unroll
+        for (int c = 0; c < STAGES - 1; ++c)
+            if (DIAG != 1 || c == 0)
+                if (c < g.NC) issue(c, c);
+        for (int c = 0; c < g.NC; ++c) {
+            const int st = c % STAGES;
+            // chunk c landed (the STAGES-2 younger chunks may stay in flight), all waves done with chunk c-1
+            if (DIAG == 1 || c + STAGES - 2 >= g.NC) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else if constexpr (STAGES == 3) {
+                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (DIAG != 1 && c + STAGES - 1 < g.NC) issue(c + STAGES - 1, (c + STAGES - 1) % STAGES);
             bf16x8 fa[2][3], fb[2][3];
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int p = 0; p < 3; ++p) {
-                    fa[u][p] = lds[q][0][((ua + u) * 3 + p) * 64 + lane];
-                    fb[u][p] = lds[q][1][((ub + u) * 3 + p) * 64 + lane];
+                    fa[u][p] = lds[DIAG == 1 ? 0 : st][0][((ua + u) * 3 + p) * 64 + lane];
+                    fb[u][p] = lds[DIAG == 1 ? 0 : st][1][(p * 4 + gq) * 64 + 16 * (ub + u) + j];
                 }
 #pragma unroll
             for (int u = 0; u < 2; ++u)
@@ -305,17 +340,6 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
                     acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][1], acc[u][v], 0, 0, 0);
                     acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][0], acc[u][v], 0, 0, 0);
                 }
-            // stage q^1 was last read in chunk c-1, before the barrier
-            if (DIAG != 1 && c + 1 < g.NC) stash(q ^ 1, q ^ 1);
-            __syncthreads();
-        };
-        fetch(0, 0);
-        if (g.NC > 1) fetch(1, 1);
-        stash(0, 0);
-        __syncthreads();
-        for (int c = 0; c < g.NC; c += 2) {  // NC is even (Np is a multiple of 64)
-            body(c, 0);
-            body(c + 1, 1);
         }
     } else {
         const double* F = reinterpret_cast<const double*>(a.ws + g.o_frag);
@@ -357,15 +381,27 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             constexpr bool kState = DIAG != 3;
             const real4 Gv = kState ? reinterpret_cast<const real4*>(a.ws + g.o_G)[t4] : real4{0.16, 0.16, 0.16, 0.16};
             const real4 Sv = kState ? reinterpret_cast<const real4*>(a.ws + g.o_S)[t4] : real4{11, 11, 11, 11};
-            real4 Ev, Iv = kState ? Iw[t4] : real4{0.1, 0.1, 0.1, 0.1};
+            real4 Ev, Iv;
+            if constexpr (kPF) Iv = pfI[v][u];
+            else Iv = kState ? Iw[t4] : real4{0.1, 0.1, 0.1, 0.1};
             AccA<sizeof(Real) == 4> Av[4];
             real4* Xn;  // next step's E image (f64) / tile-major E (f32)
             if constexpr (sizeof(Real) == 4) {
-                const size_t x4 = x32_index(g, b, n0) >> 2;  // this lane's 4 nodes, one real4
-                Ev = reinterpret_cast<const real4*>(a.ws + (buf ? g.o_X1 : g.o_X0))[x4];
-                Xn = reinterpret_cast<real4*>(a.ws + (buf ? g.o_X0 : g.o_X1)) + x4;
-                const real4 hi = kState ? Ahw[t4] : real4{2.5, 2.5, 2.5, 2.5};
-                const real4 lo = kState ? reinterpret_cast<const real4*>(a.ws + g.o_Alo)[t4] : real4{0, 0, 0, 0};
+                // E = hi + mid + lo (exact) of this lane's 4 nodes: 8 B per part
+                const bf16x4* Xc = reinterpret_cast<const bf16x4*>(a.ws + (buf ? g.o_X1 : g.o_X0));
+                const bf16x4 eh = Xc[xs_index(g, 0, b, n0) >> 2], em = Xc[xs_index(g, 1, b, n0) >> 2],
+                             el = Xc[xs_index(g, 2, b, n0) >> 2];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) Ev[r] = ((float)eh[r] + (float)em[r]) + (float)el[r];
+                Xn = nullptr;
+                real4 hi, lo;
+                if constexpr (kPF) {
+                    hi = pfH[v][u];
+                    lo = pfL[v][u];
+                } else {
+                    hi = kState ? Ahw[t4] : real4{2.5, 2.5, 2.5, 2.5};
+                    lo = kState ? reinterpret_cast<const real4*>(a.ws + g.o_Alo)[t4] : real4{0, 0, 0, 0};
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     Av[r].hi = hi[r];
@@ -416,7 +452,13 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             }
             if (kState) Iw[t4] = In;
             if constexpr (sizeof(Real) == 4) {
-                *Xn = En;
+                // next step's B operand: the exact 3-way split of the new E
+                float ev[4] = {En[0], En[1], En[2], En[3]};
+                bf16x4 ph[3];
+                split3(ev, ph[0], ph[1], ph[2]);
+                bf16x4* Xo = reinterpret_cast<bf16x4*>(a.ws + (buf ? g.o_X0 : g.o_X1));
+#pragma unroll
+                for (int p = 0; p < 3; ++p) Xo[xs_index(g, p, b, n0) >> 2] = ph[p];
                 if (!kState) continue;
                 real4 hi, lo;
 #pragma unroll
@@ -437,7 +479,7 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
     }
 }
 
-template <typename Real, int DIAG = 0>
+template <typename Real, int DIAG = 0, int STAGES = 2, bool PF = false>
 int run_large(const wc_params* p, int B, int N, const double* sc, const double* G, const double* sigmaE,
               const uint64_t* keys, double* E, double* I, double* A, int64_t step0, int64_t nsteps, double tau_ip,
               int64_t rec_every, int64_t rec_ld, void* recE, void* recI, void* recA, void* workspace,
@@ -465,7 +507,8 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
     const int W = (g.Bp / kTile) * (g.Np / kTile);
     for (int64_t s = 0; s < nsteps; ++s) {
         const int rec_row = (rec_every > 0 && s % rec_every == 0) ? (int)(s / rec_every) : -1;
-        hipLaunchKernelGGL((step_kernel<Real, DIAG>), dim3(W), dim3(256), 0, st, a, (int)s, rec_row, (int)(s & 1));
+        hipLaunchKernelGGL((step_kernel<Real, DIAG, STAGES, PF>), dim3(W), dim3(256), 0, st, a, (int)s, rec_row,
+                           (int)(s & 1));
     }
     const size_t bn = (size_t)B * N;
     hipLaunchKernelGGL(finish_kernel<Real>, dim3((unsigned)((bn + 255) / 256)), dim3(256), 0, st, a,
@@ -503,6 +546,10 @@ int wc_large_diag(int variant, const wc_params* p, int B, int N, const double* s
                                              nullptr, nullptr, nullptr, workspace, st);
         case 103: return run_large<float, 3>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, 0, 0,
                                              nullptr, nullptr, nullptr, workspace, st);
+        case 104: return run_large<float, 0, 3, true>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip,
+                                                      0, 0, nullptr, nullptr, nullptr, workspace, st);
+        case 105: return run_large<float, 0, 2, true>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip,
+                                                      0, 0, nullptr, nullptr, nullptr, workspace, st);
         default: return wc_set_err(WC_EINVAL, "unknown large-N diagnostic variant");
     }
 }

@@ -23,7 +23,7 @@ def main():
     rng = np.random.default_rng(0)
     bt = Batch(sc, 0.16 + rng.uniform(-0.1, 0.3, B), 7.68 + rng.uniform(-0.2, 0.2, B),
                sim_keys(np.arange(B), np.zeros(B, dtype=np.int64)), precision="f32")
-    variants = [100, 101, 102, 103]
+    variants = [100, 101, 102, 103, 104, 105]
     times = {v: [] for v in variants}
     for r in range(3):
         for v in variants:
