@@ -176,3 +176,28 @@ def test_pipeline_short_schedule_vs_oracle(cuda, sc90):
                 assert cols[name][b] == v, (name, cols[name][b], v)
             else:
                 np.testing.assert_allclose(cols[name][b], v, rtol=1e-6, atol=1e-8, err_msg=name)
+
+
+def test_pipeline_fc_ssim_vs_oracle(cuda, sc90):
+    """North star: FC SSIM >= 0.999 vs the reference at fixed seed.  At fixed seed
+    this is the fp64 path (the oracle restates the reference loop with the same
+    Philox stream); it holds to ~1e-9.  The fp32 product path cannot be compared
+    pathwise over a sweep horizon: the SDE is chaotic (a 1e-7 difference grows
+    ~10x per 0.1 s of model time, tests/test_sde_gpu.py), so fp32 and fp64
+    realisations of the same seed decorrelate -- it is validated statistically
+    against the shipped tables instead."""
+    from nremmodfc_amd.model import Schedule, driver_params, sim_keys
+    from nremmodfc_amd.pipeline import run_sweep
+    sch = Schedule(n_trans1=200, n_trans2=2000, n_sim=400_000)  # 18 BOLD samples
+    G = np.array([0.16, 0.10, 0.22, 0.16])
+    S = np.array([7.68, 7.50, 7.80, 7.88])
+    keys = sim_keys([0, 1, 2, 3], [0, 5, 9, 11])
+    emp = {s: datasets.load_empfc(s) for s in datasets.STATES}
+    res = run_sweep(sc90, G, S, keys, emp, sch, precision="f64", want_fc=True)
+    ob = oracle.OracleBatch(sc90, G, S, keys, driver_params())
+    ob.integrate(sch.n_trans1, 0.05)
+    ob.integrate(sch.n_trans2, 1.0)
+    rec = ob.integrate(sch.n_sim, 2.0, 20)
+    for b in range(len(keys)):
+        _, _, wfc = osg.sim_metrics(rec[b], emp)
+        assert osg.ssim(res.fc[b], wfc, data_range=2.0) >= 0.999999
