@@ -183,7 +183,7 @@ def test_pipeline_fc_ssim_vs_oracle(cuda, sc90):
     this is the fp64 path (the oracle restates the reference loop with the same
     Philox stream); it holds to ~1e-9.  The fp32 product path cannot be compared
     pathwise over a sweep horizon: the SDE is chaotic (a 1e-7 difference grows
-    ~10x per 0.1 s of model time, tests/test_sde_gpu.py), so fp32 and fp64
+    ~1e4-fold per second of model time, tests/test_sde_gpu.py), so fp32 and fp64
     realisations of the same seed decorrelate -- it is validated statistically
     against the shipped tables instead."""
     from nremmodfc_amd.model import Schedule, driver_params, sim_keys
