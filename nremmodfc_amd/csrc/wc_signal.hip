@@ -76,6 +76,22 @@ struct BoldArgs {
 
 // forward output y of data sample k: accumulate the block's zero-state backward
 // summaries; at the block's last sample store them (block m = k / dec)
+// (r, m) = (k % dec, k / dec), passed in by the caller's running counters
+__device__ __forceinline__ void emit_rm(const BoldArgs& a, const BoldLayout& L, double* st, int64_t c, int64_t k,
+                                        int64_t r, int64_t m, double y, double acc[5]) {
+    const int64_t dec = a.cfg.dec;
+    const double* tab = st + L.tab + 5 * r;  // wave-uniform address: scalar loads
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[j] += tab[j] * y;
+    if (r == dec - 1 || k == a.n - 1) {
+        st[L.yzs + m * L.C + c] = acc[0];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) st[L.u + (m * 4 + j) * L.C + c] = acc[1 + j];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc[j] = 0.0;
+    }
+}
+
 __device__ __forceinline__ void emit(const BoldArgs& a, const BoldLayout& L, double* st, int64_t c, int64_t k,
                                      double y, double acc[5]) {
     const int64_t dec = a.cfg.dec;
@@ -150,6 +166,16 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
     for (int k = 0; k < 5; ++k) acc[k] = st[L.acc + k * a.C + cc];
     const int64_t neq = a.cfg.neq, n = a.n;
     const double dt = a.cfg.dt;
+    // (r_blk, m_blk) = ((t - neq) % dec, (t - neq) / dec) of the next sample with
+    // t >= neq, advanced by one per sample (no 64-bit division in the loop)
+    int64_t r_blk = 0, m_blk = 0;
+    {
+        const int64_t i0 = t0 - neq;
+        if (i0 > 0) {
+            r_blk = i0 % a.cfg.dec;
+            m_blk = i0 / a.cfg.dec;
+        }
+    }
     // one sample of the stream (x = E at sample tt of this chunk)
     auto sample = [&](double x, int64_t tt) {
         const int64_t t = t0 + tt;
@@ -188,6 +214,11 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
         q += dt * dq;
         if (t < neq) return;
         const int64_t i = t - neq;  // data index of this BOLD sample
+        const int64_t r_cur = r_blk, m_cur = m_blk;
+        if (++r_blk == a.cfg.dec) {
+            r_blk = 0;
+            ++m_blk;
+        }
         if (i >= n) return;
         if (i >= n - 16) st[L.x16 + (i - (n - 16)) * a.C + c] = bold;
         if (i < 16) st[L.head + i * a.C + c] = bold;
@@ -201,7 +232,7 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
             for (int k = 15; k >= 1; --k) iir_step(zf, 2.0 * x0 - st[L.head + k * a.C + c], b, fa);
             for (int k = 0; k <= 15; ++k) emit(a, L, st, c, k, iir_step(zf, st[L.head + k * a.C + c], b, fa), acc);
         } else {
-            emit(a, L, st, c, i, iir_step(zf, bold, b, fa), acc);
+            emit_rm(a, L, st, c, i, r_cur, m_cur, iir_step(zf, bold, b, fa), acc);
         }
         if (i == n - 1) {
             // odd extension at the end: 2 x[n-1] - x[n-2..n-16]; backward pass starts there
