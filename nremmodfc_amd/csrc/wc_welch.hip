@@ -48,7 +48,12 @@ __global__ void twiddle_kernel(double* tw) {
     tw[2 * m] = c;
     tw[2 * m + 1] = -s;
     float2* tw32 = reinterpret_cast<float2*>(tw + 2 * kSeg);
-    tw32[m] = make_float2((float)c, (float)-s);
+    // fp32 half turn by symmetry, T[m + 2000] = -T[m] exactly, so the product kernel can
+    // keep only the first half in LDS
+    if (m < kFFT) {
+        tw32[m] = make_float2((float)c, (float)-s);
+        tw32[m + kFFT] = make_float2(-(float)c, (float)s);
+    }
     // periodic Hann pairs for the packed samples (2j, 2j+1): hann2[j] = (w(2j), w(2j+1))
     if ((m & 1) == 0) {
         double s1, c1;
@@ -240,6 +245,10 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
 constexpr int kWv = 4;
 typedef __attribute__((address_space(3))) void* lds_vptr;
 constexpr int kLaneBins = (kBins + 63) / 64;  // 32
+#ifndef WC_WELCH_PF_EARLY
+#define WC_WELCH_PF_EARLY 10
+#endif
+constexpr int kPfEarly = WC_WELCH_PF_EARLY;  // float4 of the next column fetched right after stage 1
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -253,53 +262,64 @@ __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
 
 // in-place radix-RAD Stockham stage (p = product of the previous radices);
 // WIN: stage 1 also detrends and Hann-windows the raw packed samples it reads
+// T^j = exp(-2 pi i j / 4000), j in [0, 4000), from the LDS half table (T^(j+2000) = -T^j)
+__device__ __forceinline__ float2 twh(const float2* T, int j) {
+    const bool hi = j >= kFFT;
+    float2 w = T[hi ? j - kFFT : j];
+    if (hi) w = make_float2(-w.x, -w.y);
+    return w;
+}
+
 template <int RAD, int P, bool WIN>
-__device__ __forceinline__ void wstage(float2* z, const float2* __restrict__ tw, int lane) {
+__device__ __forceinline__ void wstage(float2* z, const float2* T, const float2* __restrict__ hann, int lane) {
     constexpr int S = kFFT / RAD;
     constexpr int NB = (S + 63) / 64;
     constexpr int TS = 2 * (kFFT / (P * RAD));  // twiddle index step in the 4000-table
+    // every read is unconditional (the lanes of a partial last row read the row's last
+    // butterfly again, index clamped); only the writes of that row are masked
     float2 u[NB][RAD];
     float part = 0.f;
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
-        const int i = lane + 64 * q;
-        if (i < S) {
+        const int i = 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1);
+        const bool own = 64 * (q + 1) <= S || lane + 64 * q < S;
 #pragma unroll
-            for (int r = 0; r < RAD; ++r) {
-                u[q][r] = z[i + r * S];
-                if constexpr (WIN) part += u[q][r].x + u[q][r].y;
-            }
+        for (int r = 0; r < RAD; ++r) {
+            u[q][r] = z[i + r * S];
+            if constexpr (WIN) part += own ? u[q][r].x + u[q][r].y : 0.f;
         }
     }
     if constexpr (WIN) {
         // the first stage reads every raw sample: column mean (constant detrend), then
         // the periodic Hann window w(t) = 0.5 - 0.5 cos(2 pi t / 4000) on the packed pairs
+        float2 hw[NB][RAD];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const int i = 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1);
+#pragma unroll
+            for (int r = 0; r < RAD; ++r) hw[q][r] = hann[i + r * S];  // (w(2m), w(2m+1))
+        }
         for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
         const float mean = part / (float)kSeg;
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-            __builtin_amdgcn_sched_barrier(0);  // window-table loads: bounded look-ahead
-            const int i = lane + 64 * q;
-            if (i < S) {
 #pragma unroll
-                for (int r = 0; r < RAD; ++r) {
-                    const float2 w = tw[kSeg + i + r * S];  // (w(2m), w(2m+1)) of the Hann table after the twiddles
-                    u[q][r].x = (u[q][r].x - mean) * w.x;
-                    u[q][r].y = (u[q][r].y - mean) * w.y;
-                }
+            for (int r = 0; r < RAD; ++r) {
+                u[q][r].x = (u[q][r].x - mean) * hw[q][r].x;
+                u[q][r].y = (u[q][r].y - mean) * hw[q][r].y;
             }
         }
     }
     wave_sync();
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
-        __builtin_amdgcn_sched_barrier(0);  // bound the twiddle-load look-ahead (register pressure)
-        const int i = lane + 64 * q;
-        if (i < S) {
+        const int i = 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1);
+        const bool own = 64 * (q + 1) <= S || lane + 64 * q < S;
+        {
             const int k = i % P;
             if constexpr (P > 1) {  // first stage: every twiddle is 1
 #pragma unroll
-                for (int r = 1; r < RAD; ++r) u[q][r] = cmulf(u[q][r], tw[r * k * TS]);
+                for (int r = 1; r < RAD; ++r) u[q][r] = cmulf(u[q][r], twh(T, r * k * TS));
             }
             float2 U[RAD];
             if constexpr (RAD == 4) {
@@ -329,8 +349,10 @@ __device__ __forceinline__ void wstage(float2* z, const float2* __restrict__ tw,
                 U[3] = make_float2(a2.x - b2.y, a2.y + b2.x);
             }
             const int j = (i - k) * RAD + k;
+            if (own) {
 #pragma unroll
-            for (int s2i = 0; s2i < RAD; ++s2i) z[j + s2i * P] = U[s2i];
+                for (int s2i = 0; s2i < RAD; ++s2i) z[j + s2i * P] = U[s2i];
+            }
         }
     }
     wave_sync();
@@ -342,7 +364,9 @@ __global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float2* z = reinterpret_cast<float2*>(smem) + w * kFFT;
     float* zf = reinterpret_cast<float*>(z);
+    float2* T = reinterpret_cast<float2*>(smem) + kWv * kFFT;  // twiddle half table, shared by the waves
     const float2* tw = reinterpret_cast<const float2*>(a.tw + 2 * kSeg);
+    const float2* hann = tw + kSeg;
     const float* E = static_cast<const float*>(a.E);
     float acc[kLaneBins];
 #pragma unroll
@@ -363,46 +387,59 @@ __global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs
             }
         }
     }
+    // the column's 4000 samples as 16 float4 per lane (t = 256 i + 4 lane; each lane's 16 B
+    // lie in one ring run); the next column is fetched into these registers while the
+    // current one is transformed, so the FFT never waits on HBM
+    // (branch-free: lanes past the segment end re-read its last 16 B, and the last
+    // wave-column re-fetches itself, an L2 hit, so every load is unconditional)
+    typedef float f4v __attribute__((ext_vector_type(4)));  // (native vector: HIP's float4 struct copies stay in scratch)
+    f4v pf[16];
+#define WELCH_FETCH(n, I0, I1)                                                                 \
+    {                                                                                          \
+        const float* col_ = E + ((int64_t)b * a.N + (n)) * a.ld;                               \
+        _Pragma("unroll") for (int i = I0; i < I1; ++i) {                                      \
+            const int t = min(256 * i + 4 * lane, kSeg - 4);                                   \
+            int off = ro[0] + t;                                                               \
+            _Pragma("unroll") for (int r = 1; r < 5; ++r) off = t >= rt[r] ? ro[r] + t : off;  \
+            pf[i] = *reinterpret_cast<const f4v*>(col_ + off);                                 \
+        }                                                                                      \
+    }
+    WELCH_FETCH(min(w, a.N - 1), 0, 16);
+    for (int i = threadIdx.x; i < kFFT / 2; i += kWv * 64)
+        reinterpret_cast<float4*>(T)[i] = reinterpret_cast<const float4*>(tw)[i];
+    __syncthreads();
 
     for (int n = w; n < a.N; n += kWv) {
-        // ---- stage the raw segment into LDS by LDS-DMA: 16 x global_load_lds_dwordx4
-        //      (1 KB per wave instruction); each lane's 16 B lie in one ring run ----
-        const float* col = E + ((int64_t)b * a.N + n) * a.ld;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int t = 256 * i + 4 * lane;
-            if (t < kSeg) {
-                int off = ro[0] + t;
-#pragma unroll
-                for (int r = 1; r < 5; ++r)
-                    if (t >= rt[r]) off = ro[r] + t;
-                __builtin_amdgcn_global_load_lds(col + off, (lds_vptr)(zf + 256 * i), 16, 0, 0);
-            }
+            if (256 * (i + 1) <= kSeg || t < kSeg) *reinterpret_cast<f4v*>(zf + t) = pf[i];
         }
-        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0): the DMA has landed
         wave_sync();
         // ---- Stockham 2000 = 5 * 5 * 5 * 4 * 4, window fused into the first stage ----
-        // (the twiddle base is laundered per column so the compiler does not hoist
-        // hundreds of loop-invariant 64-bit table addresses out of the column loop)
-        const float2* twl = tw;
+        // (the lane id is laundered per column so the compiler does not hoist hundreds
+        // of loop-invariant twiddle offsets out of the column loop)
         int ln = lane;
-        asm volatile("" : "+s"(twl), "+v"(ln));
-        wstage<5, 1, true>(z, twl, ln);
-        wstage<5, 5, false>(z, twl, ln);
-        wstage<5, 25, false>(z, twl, ln);
-        wstage<4, 125, false>(z, twl, ln);
-        wstage<4, 500, false>(z, twl, ln);
+        asm volatile("" : "+v"(ln));
+        wstage<5, 1, true>(z, T, hann, ln);
+        // the Hann loads have retired: the next column's loads are the only VMEM in flight
+        const int nn = n + kWv < a.N ? n + kWv : n;
+        WELCH_FETCH(nn, 0, kPfEarly);
+        wstage<5, 5, false>(z, T, hann, ln);
+        wstage<5, 25, false>(z, T, hann, ln);
+        wstage<4, 125, false>(z, T, hann, ln);
+        wstage<4, 500, false>(z, T, hann, ln);
+        WELCH_FETCH(nn, kPfEarly, 16);  // (the rest of the next column: fewer live registers through the stages)
         // ---- unpack X_k = (Z_k + conj Z_-k)/2 - i/2 W^k (Z_k - conj Z_-k), |X_k|^2 ----
 #pragma unroll
         for (int i = 0; i < kLaneBins; ++i) {
-            if ((i & 3) == 0) __builtin_amdgcn_sched_barrier(0);
             const int k = ln + 64 * i;
             if (k < kBins) {
                 const float2 Zk = z[k == kFFT ? 0 : k];
                 const float2 Zc = z[k == 0 ? 0 : kFFT - k];
                 const float er = 0.5f * (Zk.x + Zc.x), ei = 0.5f * (Zk.y - Zc.y);
                 const float dr = Zk.x - Zc.x, di = Zk.y + Zc.y;
-                const float2 W = twl[k];
+                const float2 W = twh(T, k);
                 const float pr = W.x * dr - W.y * di, pi = W.x * di + W.y * dr;
                 const float xr = er + 0.5f * pi, xi = ei - 0.5f * pr;
                 acc[i] += xr * xr + xi * xi;
@@ -410,6 +447,7 @@ __global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs
         }
         wave_sync();  // the next column overwrites z
     }
+#undef WELCH_FETCH
     // ---- combine the waves (fp64) into the simulation's accumulator row (single writer) ----
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [kWv][kBins]
@@ -492,7 +530,10 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
         hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
     } else {
         if (ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 && ld < INT32_MAX / 2) {
-            const size_t lds = (size_t)kWv * kFFT * sizeof(float2);  // 64,000 B
+            const size_t lds = (size_t)(kWv + 1) * kFFT * sizeof(float2);  // 80,000 B: 2 workgroups per CU
+            hipError_t ea = hipFuncSetAttribute((const void*)welch_wave_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
             hipLaunchKernelGGL(welch_wave_kernel, dim3(B), dim3(kWv * 64), lds, st, a);
         } else {  // unaligned rings (e.g. odd lengths): the LDS-Stockham kernel, scalar loads
             const size_t lds = (size_t)2 * kG<float> * kFFT * sizeof(cx<float>) + 4 * kG<float> * sizeof(float);
