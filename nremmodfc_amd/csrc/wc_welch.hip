@@ -238,17 +238,45 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
 // Each wave owns one column's 2000-point packed FFT in its own 16 KB of LDS and
 // runs it with no workgroup barrier: every radix stage reads all of the wave's
 // butterfly inputs into registers, then writes the outputs in place (the wave
-// owns every point).  Four waves (columns) per workgroup, 64 KB of LDS, two
-// workgroups per CU.  fp32 arithmetic with the correctly rounded fp32 twiddle
-// table; |X_k|^2 summed per lane in fp32 over the wave's ~N/4 columns, then the
-// four waves are combined in fp64 and added to the simulation's fp64 row.
-constexpr int kWv = 4;
-typedef __attribute__((address_space(3))) void* lds_vptr;
+// owns every point).  Eight waves per workgroup, four per simulation (two
+// simulations per workgroup), one workgroup per CU: 8 x 16 KB of columns plus
+// 32 KB of twiddle tables shared by the eight waves (per-stage tables laid out
+// [k][r], so a butterfly's twiddles are consecutive and need no index
+// arithmetic beyond k).  While a column is transformed, the wave's next column
+// is already on its way from HBM into registers, so the FFT never waits on
+// memory.  fp32 arithmetic with the correctly rounded fp32 twiddle table;
+// |X_k|^2 summed per lane in fp32 over the wave's ~N/4 columns, then the four
+// waves of a simulation are combined in fp64 and added to its fp64 row.
+constexpr int kWv = 4;       // waves (columns in flight) per simulation
+constexpr int kSimsWg = 2;   // simulations per workgroup
 constexpr int kLaneBins = (kBins + 63) / 64;  // 32
 #ifndef WC_WELCH_PF_EARLY
 #define WC_WELCH_PF_EARLY 10
 #endif
 constexpr int kPfEarly = WC_WELCH_PF_EARLY;  // float4 of the next column fetched right after stage 1
+// per-stage twiddle tables: entry (k, r) = T^(r k TS) at base + k (RAD - 1) + r - 1
+constexpr int kTb2 = 0, kTb3 = kTb2 + 5 * 4, kTb4 = kTb3 + 25 * 4, kTb5 = kTb4 + 125 * 3;
+constexpr int kStageTw = kTb5 + 500 * 3;  // 1995
+constexpr int kUnpTw = kBins + 1;         // T^k, k in [0, 2000] (+1 pad: 16-B aligned stage tables)
+constexpr size_t kWelchLds = (size_t)kWv * kSimsWg * kFFT * 8 + (size_t)(kUnpTw + kStageTw) * 8;  // 159,976 B
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// stage tables from the fp32 turn (run after twiddle_kernel): entry (k, r) of the
+// stage with (P, RAD) is T^(r k TS), TS = 2 kFFT / (P RAD), r k TS < 4000
+__global__ void stage_twiddle_kernel(double* tw) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= kStageTw) return;
+    const float2* tw32 = reinterpret_cast<const float2*>(tw + 2 * kSeg);
+    float2* st = const_cast<float2*>(tw32) + kSeg + kFFT;
+    int base, P, RAD;
+    if (m < kTb3) { base = kTb2; P = 5; RAD = 5; }
+    else if (m < kTb4) { base = kTb3; P = 25; RAD = 5; }
+    else if (m < kTb5) { base = kTb4; P = 125; RAD = 4; }
+    else { base = kTb5; P = 500; RAD = 4; }
+    const int k = (m - base) / (RAD - 1), r = (m - base) % (RAD - 1) + 1;
+    st[m] = tw32[r * k * (2 * kFFT / (P * RAD))];
+}
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -256,28 +284,38 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
-    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+// Packed complex helpers written with explicit VOP3P modifiers (op_sel picks the
+// register half each result lane reads, neg_lo/neg_hi negate per lane): the compiler
+// does not fold a one-lane negation into the modifiers and would emit xor + mov pairs.
+__device__ __forceinline__ f2 cmulv(f2 u, f2 w) {  // u * w in two packed ops
+    f2 t, r;
+    // t = (u.x w.x, u.x w.y)
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(u), "v"(w));
+    // r = (-u.y w.y + t.x, u.y w.x + t.y)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(u), "v"(w), "v"(t));
+    return r;
+}
+__device__ __forceinline__ f2 add_mi(f2 a, f2 d) {  // a - i d = (a.x + d.y, a.y - d.x)
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(d));
+    return r;
+}
+__device__ __forceinline__ f2 sub_mi(f2 a, f2 d) {  // a + i d = (a.x - d.y, a.y + d.x)
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(d));
+    return r;
 }
 
-// in-place radix-RAD Stockham stage (p = product of the previous radices);
-// WIN: stage 1 also detrends and Hann-windows the raw packed samples it reads
-// T^j = exp(-2 pi i j / 4000), j in [0, 4000), from the LDS half table (T^(j+2000) = -T^j)
-__device__ __forceinline__ float2 twh(const float2* T, int j) {
-    const bool hi = j >= kFFT;
-    float2 w = T[hi ? j - kFFT : j];
-    if (hi) w = make_float2(-w.x, -w.y);
-    return w;
-}
-
-template <int RAD, int P, bool WIN>
-__device__ __forceinline__ void wstage(float2* z, const float2* T, const float2* __restrict__ hann, int lane) {
+// in-place radix-RAD Stockham stage (P = product of the previous radices, TB its
+// twiddle table base); WIN: stage 1 also detrends and Hann-windows the raw packed
+// samples it reads.  Every read is unconditional (the lanes of a partial last row
+// re-read the row's last butterfly, index clamped); only that row's writes are masked.
+template <int RAD, int P, int TB, bool WIN>
+__device__ __forceinline__ void wstage(f2* z, const f2* Ts, const f2* __restrict__ hann, int lane) {
     constexpr int S = kFFT / RAD;
     constexpr int NB = (S + 63) / 64;
-    constexpr int TS = 2 * (kFFT / (P * RAD));  // twiddle index step in the 4000-table
-    // every read is unconditional (the lanes of a partial last row read the row's last
-    // butterfly again, index clamped); only the writes of that row are masked
-    float2 u[NB][RAD];
+    f2 u[NB][RAD];
     float part = 0.f;
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
@@ -292,7 +330,7 @@ __device__ __forceinline__ void wstage(float2* z, const float2* T, const float2*
     if constexpr (WIN) {
         // the first stage reads every raw sample: column mean (constant detrend), then
         // the periodic Hann window w(t) = 0.5 - 0.5 cos(2 pi t / 4000) on the packed pairs
-        float2 hw[NB][RAD];
+        f2 hw[NB][RAD];
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
             const int i = 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1);
@@ -302,71 +340,64 @@ __device__ __forceinline__ void wstage(float2* z, const float2* T, const float2*
         for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
         const float mean = part / (float)kSeg;
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
+        for (int q = 0; q < NB; ++q)
 #pragma unroll
-            for (int r = 0; r < RAD; ++r) {
-                u[q][r].x = (u[q][r].x - mean) * hw[q][r].x;
-                u[q][r].y = (u[q][r].y - mean) * hw[q][r].y;
-            }
-        }
+            for (int r = 0; r < RAD; ++r) u[q][r] = (u[q][r] - mean) * hw[q][r];
     }
     wave_sync();
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
         const int i = 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1);
         const bool own = 64 * (q + 1) <= S || lane + 64 * q < S;
-        {
-            const int k = i % P;
-            if constexpr (P > 1) {  // first stage: every twiddle is 1
+        const int k = i % P;
+        if constexpr (P > 1) {  // first stage: every twiddle is 1
+            const f2* tp = Ts + TB + k * (RAD - 1);
 #pragma unroll
-                for (int r = 1; r < RAD; ++r) u[q][r] = cmulf(u[q][r], twh(T, r * k * TS));
-            }
-            float2 U[RAD];
-            if constexpr (RAD == 4) {
-                const float2 a = make_float2(u[q][0].x + u[q][2].x, u[q][0].y + u[q][2].y);
-                const float2 b = make_float2(u[q][0].x - u[q][2].x, u[q][0].y - u[q][2].y);
-                const float2 c = make_float2(u[q][1].x + u[q][3].x, u[q][1].y + u[q][3].y);
-                const float2 d = make_float2(u[q][1].x - u[q][3].x, u[q][1].y - u[q][3].y);
-                U[0] = make_float2(a.x + c.x, a.y + c.y);
-                U[2] = make_float2(a.x - c.x, a.y - c.y);
-                U[1] = make_float2(b.x + d.y, b.y - d.x);  // b - i d
-                U[3] = make_float2(b.x - d.y, b.y + d.x);  // b + i d
-            } else {
-                const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
-                const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
-                const float2 t1 = make_float2(u[q][1].x + u[q][4].x, u[q][1].y + u[q][4].y);
-                const float2 t2 = make_float2(u[q][2].x + u[q][3].x, u[q][2].y + u[q][3].y);
-                const float2 t3 = make_float2(u[q][1].x - u[q][4].x, u[q][1].y - u[q][4].y);
-                const float2 t4 = make_float2(u[q][2].x - u[q][3].x, u[q][2].y - u[q][3].y);
-                U[0] = make_float2(u[q][0].x + t1.x + t2.x, u[q][0].y + t1.y + t2.y);
-                const float2 a1 = make_float2(u[q][0].x + c1 * t1.x + c2 * t2.x, u[q][0].y + c1 * t1.y + c2 * t2.y);
-                const float2 a2 = make_float2(u[q][0].x + c2 * t1.x + c1 * t2.x, u[q][0].y + c2 * t1.y + c1 * t2.y);
-                const float2 b1 = make_float2(s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y);
-                const float2 b2 = make_float2(s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y);
-                U[1] = make_float2(a1.x + b1.y, a1.y - b1.x);
-                U[4] = make_float2(a1.x - b1.y, a1.y + b1.x);
-                U[2] = make_float2(a2.x + b2.y, a2.y - b2.x);
-                U[3] = make_float2(a2.x - b2.y, a2.y + b2.x);
-            }
-            const int j = (i - k) * RAD + k;
-            if (own) {
+            for (int r = 1; r < RAD; ++r) u[q][r] = cmulv(u[q][r], tp[r - 1]);
+        }
+        f2 U[RAD];
+        if constexpr (RAD == 4) {
+            const f2 a = u[q][0] + u[q][2], b = u[q][0] - u[q][2];
+            const f2 c = u[q][1] + u[q][3], d = u[q][1] - u[q][3];
+            U[0] = a + c;
+            U[2] = a - c;
+            U[1] = add_mi(b, d);  // b - i d
+            U[3] = sub_mi(b, d);  // b + i d
+        } else {
+            const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+            const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+            const f2 t1 = u[q][1] + u[q][4], t2 = u[q][2] + u[q][3];
+            const f2 t3 = u[q][1] - u[q][4], t4 = u[q][2] - u[q][3];
+            U[0] = u[q][0] + t1 + t2;
+            const f2 a1 = u[q][0] + c1 * t1 + c2 * t2;
+            const f2 a2 = u[q][0] + c2 * t1 + c1 * t2;
+            const f2 b1 = s1 * t3 + s2 * t4, b2 = s2 * t3 - s1 * t4;
+            U[1] = add_mi(a1, b1);  // a1 - i b1
+            U[4] = sub_mi(a1, b1);
+            U[2] = add_mi(a2, b2);
+            U[3] = sub_mi(a2, b2);
+        }
+        const int j = (i - k) * RAD + k;
+        if (own) {
 #pragma unroll
-                for (int s2i = 0; s2i < RAD; ++s2i) z[j + s2i * P] = U[s2i];
-            }
+            for (int s2i = 0; s2i < RAD; ++s2i) z[j + s2i * P] = U[s2i];
         }
     }
     wave_sync();
 }
 
-__global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs a) {
+__global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const WelchArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int b = blockIdx.x;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float2* z = reinterpret_cast<float2*>(smem) + w * kFFT;
+    const int wg = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = wg & (kWv - 1);                         // column slot within the simulation
+    const int b = blockIdx.x * kSimsWg + wg / kWv;        // this wave's simulation
+    const int ncol = b < a.B ? a.N : 0;
+    f2* z = reinterpret_cast<f2*>(smem) + wg * kFFT;
     float* zf = reinterpret_cast<float*>(z);
-    float2* T = reinterpret_cast<float2*>(smem) + kWv * kFFT;  // twiddle half table, shared by the waves
-    const float2* tw = reinterpret_cast<const float2*>(a.tw + 2 * kSeg);
-    const float2* hann = tw + kSeg;
+    f2* Tu = reinterpret_cast<f2*>(smem) + kWv * kSimsWg * kFFT;  // T^k for the unpack
+    f2* Ts = Tu + kUnpTw;                                          // per-stage tables
+    const float* twg = reinterpret_cast<const float*>(a.tw + 2 * kSeg);  // fp32 tables: T, Hann, stage
+    const f2* hann = reinterpret_cast<const f2*>(twg) + kSeg;
     const float* E = static_cast<const float*>(a.E);
     float acc[kLaneBins];
 #pragma unroll
@@ -389,14 +420,14 @@ __global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs
     }
     // the column's 4000 samples as 16 float4 per lane (t = 256 i + 4 lane; each lane's 16 B
     // lie in one ring run); the next column is fetched into these registers while the
-    // current one is transformed, so the FFT never waits on HBM
-    // (branch-free: lanes past the segment end re-read its last 16 B, and the last
-    // wave-column re-fetches itself, an L2 hit, so every load is unconditional)
+    // current one is transformed (branch-free: lanes past the segment end re-read its last
+    // 16 B, and a wave's last column re-fetches itself, an L2 hit)
     typedef float f4v __attribute__((ext_vector_type(4)));  // (native vector: HIP's float4 struct copies stay in scratch)
     f4v pf[16];
+    const int64_t bc = (int64_t)min(b, a.B - 1) * a.N;
 #define WELCH_FETCH(n, I0, I1)                                                                 \
     {                                                                                          \
-        const float* col_ = E + ((int64_t)b * a.N + (n)) * a.ld;                               \
+        const float* col_ = E + (bc + (n)) * a.ld;                                             \
         _Pragma("unroll") for (int i = I0; i < I1; ++i) {                                      \
             const int t = min(256 * i + 4 * lane, kSeg - 4);                                   \
             int off = ro[0] + t;                                                               \
@@ -405,11 +436,15 @@ __global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs
         }                                                                                      \
     }
     WELCH_FETCH(min(w, a.N - 1), 0, 16);
-    for (int i = threadIdx.x; i < kFFT / 2; i += kWv * 64)
-        reinterpret_cast<float4*>(T)[i] = reinterpret_cast<const float4*>(tw)[i];
+    {  // twiddle tables into LDS: T^0..T^2000 and the stage tables (the pad entry is never read)
+        const f2* src = reinterpret_cast<const f2*>(twg);
+        const f2* sst = reinterpret_cast<const f2*>(twg) + kSeg + kFFT;
+        for (int i = threadIdx.x; i < kUnpTw + kStageTw; i += kWv * kSimsWg * 64)
+            Tu[i] = i < kBins ? src[i] : i < kUnpTw ? (f2){0.f, 0.f} : sst[i - kUnpTw];
+    }
     __syncthreads();
 
-    for (int n = w; n < a.N; n += kWv) {
+    for (int n = w; n < ncol; n += kWv) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int t = 256 * i + 4 * lane;
@@ -421,25 +456,25 @@ __global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs
         // of loop-invariant twiddle offsets out of the column loop)
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        wstage<5, 1, true>(z, T, hann, ln);
+        wstage<5, 1, 0, true>(z, Ts, hann, ln);
         // the Hann loads have retired: the next column's loads are the only VMEM in flight
-        const int nn = n + kWv < a.N ? n + kWv : n;
+        const int nn = n + kWv < ncol ? n + kWv : n;
         WELCH_FETCH(nn, 0, kPfEarly);
-        wstage<5, 5, false>(z, T, hann, ln);
-        wstage<5, 25, false>(z, T, hann, ln);
-        wstage<4, 125, false>(z, T, hann, ln);
-        wstage<4, 500, false>(z, T, hann, ln);
+        wstage<5, 5, kTb2, false>(z, Ts, hann, ln);
+        wstage<5, 25, kTb3, false>(z, Ts, hann, ln);
+        wstage<4, 125, kTb4, false>(z, Ts, hann, ln);
+        wstage<4, 500, kTb5, false>(z, Ts, hann, ln);
         WELCH_FETCH(nn, kPfEarly, 16);  // (the rest of the next column: fewer live registers through the stages)
         // ---- unpack X_k = (Z_k + conj Z_-k)/2 - i/2 W^k (Z_k - conj Z_-k), |X_k|^2 ----
 #pragma unroll
         for (int i = 0; i < kLaneBins; ++i) {
             const int k = ln + 64 * i;
             if (k < kBins) {
-                const float2 Zk = z[k == kFFT ? 0 : k];
-                const float2 Zc = z[k == 0 ? 0 : kFFT - k];
+                const f2 Zk = z[k == kFFT ? 0 : k];
+                const f2 Zc = z[k == 0 ? 0 : kFFT - k];
                 const float er = 0.5f * (Zk.x + Zc.x), ei = 0.5f * (Zk.y - Zc.y);
                 const float dr = Zk.x - Zc.x, di = Zk.y + Zc.y;
-                const float2 W = twh(T, k);
+                const f2 W = Tu[k];
                 const float pr = W.x * dr - W.y * di, pi = W.x * di + W.y * dr;
                 const float xr = er + 0.5f * pi, xi = ei - 0.5f * pr;
                 acc[i] += xr * xr + xi * xi;
@@ -448,20 +483,23 @@ __global__ void __launch_bounds__(kWv * 64, 2) welch_wave_kernel(const WelchArgs
         wave_sync();  // the next column overwrites z
     }
 #undef WELCH_FETCH
-    // ---- combine the waves (fp64) into the simulation's accumulator row (single writer) ----
+    // ---- combine each simulation's four waves (fp64) into its accumulator row (single writer) ----
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [kWv][kBins]
+    float* red = reinterpret_cast<float*>(smem);  // [kSimsWg][kWv][kBins]
 #pragma unroll
     for (int i = 0; i < kLaneBins; ++i) {
         const int k = lane + 64 * i;
-        if (k < kBins) red[w * kBins + k] = acc[i];
+        if (k < kBins) red[wg * kBins + k] = acc[i];
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < kBins; k += kWv * 64) {
+    for (int idx = threadIdx.x; idx < kSimsWg * kBins; idx += kWv * kSimsWg * 64) {
+        const int sw = idx / kBins, k = idx % kBins;
+        const int bs = blockIdx.x * kSimsWg + sw;
+        if (bs >= a.B) continue;
         double sacc = 0.0;
 #pragma unroll
-        for (int v = 0; v < kWv; ++v) sacc += (double)red[v * kBins + k];
-        a.acc[(int64_t)b * kBins + k] += sacc;
+        for (int v = 0; v < kWv; ++v) sacc += (double)red[(sw * kWv + v) * kBins + k];
+        a.acc[(int64_t)bs * kBins + k] += sacc;
     }
 }
 
@@ -501,7 +539,9 @@ __global__ void welch_peak_kernel(int B, int N, int nseg, double fs, const doubl
 extern "C" {
 
 size_t wc_welch_workspace_size(void) {
-    return (size_t)kSeg * 2 * sizeof(double) + (size_t)kSeg * sizeof(float2) + (size_t)kFFT * sizeof(float2);
+    // fp64 turn, fp32 turn, fp32 Hann pairs, fp32 stage tables
+    return (size_t)kSeg * 2 * sizeof(double) + (size_t)kSeg * sizeof(float2) + (size_t)kFFT * sizeof(float2) +
+           (size_t)kStageTw * sizeof(float2);
 }
 int wc_welch_bins(void) { return kBins; }
 
@@ -510,6 +550,8 @@ int wc_welch_prepare(void* workspace, size_t ws_bytes, void* stream) {
     if (!workspace || ws_bytes < wc_welch_workspace_size()) return wc_set_err(WC_EWORKSPACE, "wc_welch_prepare");
     hipLaunchKernelGGL(twiddle_kernel, dim3((kSeg + 255) / 256), dim3(256), 0, static_cast<hipStream_t>(stream),
                        static_cast<double*>(workspace));
+    hipLaunchKernelGGL(stage_twiddle_kernel, dim3((kStageTw + 255) / 256), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), static_cast<double*>(workspace));
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
 }
@@ -530,11 +572,11 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
         hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
     } else {
         if (ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 && ld < INT32_MAX / 2) {
-            const size_t lds = (size_t)(kWv + 1) * kFFT * sizeof(float2);  // 80,000 B: 2 workgroups per CU
             hipError_t ea = hipFuncSetAttribute((const void*)welch_wave_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWelchLds);
             if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
-            hipLaunchKernelGGL(welch_wave_kernel, dim3(B), dim3(kWv * 64), lds, st, a);
+            hipLaunchKernelGGL(welch_wave_kernel, dim3((B + kSimsWg - 1) / kSimsWg), dim3(kWv * kSimsWg * 64),
+                               kWelchLds, st, a);
         } else {  // unaligned rings (e.g. odd lengths): the LDS-Stockham kernel, scalar loads
             const size_t lds = (size_t)2 * kG<float> * kFFT * sizeof(cx<float>) + 4 * kG<float> * sizeof(float);
             hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<float>,
