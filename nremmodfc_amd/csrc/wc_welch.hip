@@ -456,6 +456,7 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         // of loop-invariant twiddle offsets out of the column loop)
         int ln = lane;
         asm volatile("" : "+v"(ln));
+        ln &= 63;  // (range-known again: unsigned index arithmetic, static masks)
         wstage<5, 1, 0, true>(z, Ts, hann, ln);
         // the Hann loads have retired: the next column's loads are the only VMEM in flight
         const int nn = n + kWv < ncol ? n + kWv : n;
@@ -466,19 +467,22 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         wstage<4, 500, kTb5, false>(z, Ts, hann, ln);
         WELCH_FETCH(nn, kPfEarly, 16);  // (the rest of the next column: fewer live registers through the stages)
         // ---- unpack X_k = (Z_k + conj Z_-k)/2 - i/2 W^k (Z_k - conj Z_-k), |X_k|^2 ----
+        //      2 X_k = s - i W^k d with s = Z_k + conj Z_-k, d = Z_k - conj Z_-k; the 1/4 of
+        //      |X_k|^2 = |2 X_k|^2 / 4 is applied once, in the final fp64 combine (exact)
+        const int l6 = ln;
 #pragma unroll
         for (int i = 0; i < kLaneBins; ++i) {
-            const int k = ln + 64 * i;
-            if (k < kBins) {
-                const f2 Zk = z[k == kFFT ? 0 : k];
-                const f2 Zc = z[k == 0 ? 0 : kFFT - k];
-                const float er = 0.5f * (Zk.x + Zc.x), ei = 0.5f * (Zk.y - Zc.y);
-                const float dr = Zk.x - Zc.x, di = Zk.y + Zc.y;
-                const f2 W = Tu[k];
-                const float pr = W.x * dr - W.y * di, pi = W.x * di + W.y * dr;
-                const float xr = er + 0.5f * pi, xi = ei - 0.5f * pr;
-                acc[i] += xr * xr + xi * xi;
+            const int k = l6 + 64 * i;
+            if (64 * (i + 1) <= kBins || k < kBins) {
+                const f2 Zk = z[64 * (i + 1) <= kFFT ? k : (k == kFFT ? 0 : k)];
+                const f2 Zc = z[i > 0 ? kFFT - k : (k == 0 ? 0 : kFFT - k)];
+                f2 sv, dv;
+                asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
+                asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
+                const f2 x = add_mi(sv, cmulv(dv, Tu[k]));
+                acc[i] = fmaf(x.x, x.x, fmaf(x.y, x.y, acc[i]));
             }
+            if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // (bounded live ranges: 4 bins at a time)
         }
         wave_sync();  // the next column overwrites z
     }
@@ -499,7 +503,7 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         double sacc = 0.0;
 #pragma unroll
         for (int v = 0; v < kWv; ++v) sacc += (double)red[(sw * kWv + v) * kBins + k];
-        a.acc[(int64_t)bs * kBins + k] += sacc;
+        a.acc[(int64_t)bs * kBins + k] += 0.25 * sacc;
     }
 }
 
