@@ -241,8 +241,8 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
 // owns every point).  Eight waves per workgroup, four per simulation (two
 // simulations per workgroup), one workgroup per CU: 8 x 16 KB of columns plus
 // 32 KB of twiddle tables shared by the eight waves (per-stage tables laid out
-// [k][r], so a butterfly's twiddles are consecutive and need no index
-// arithmetic beyond k).  While a column is transformed, the wave's next column
+// [r][k], so a row's lanes read consecutive entries and need no index arithmetic
+// beyond k).  While a column is transformed, the wave's next column
 // is already on its way from HBM into registers, so the FFT never waits on
 // memory.  fp32 arithmetic with the correctly rounded fp32 twiddle table;
 // |X_k|^2 summed per lane in fp32 over the wave's ~N/4 columns, then the four
@@ -254,7 +254,8 @@ constexpr int kLaneBins = (kBins + 63) / 64;  // 32
 #define WC_WELCH_PF_EARLY 10
 #endif
 constexpr int kPfEarly = WC_WELCH_PF_EARLY;  // float4 of the next column fetched right after stage 1
-// per-stage twiddle tables: entry (k, r) = T^(r k TS) at base + k (RAD - 1) + r - 1
+// per-stage twiddle tables: entry (k, r) = T^(r k TS) at base + (r - 1) P + k (r-major: the
+// lanes of a row read consecutive k, conflict-free; r is an immediate offset)
 constexpr int kTb2 = 0, kTb3 = kTb2 + 5 * 4, kTb4 = kTb3 + 25 * 4, kTb5 = kTb4 + 125 * 3;
 constexpr int kStageTw = kTb5 + 500 * 3;  // 1995
 constexpr int kUnpTw = kBins + 1;         // T^k, k in [0, 2000] (+1 pad: 16-B aligned stage tables)
@@ -274,7 +275,7 @@ __global__ void stage_twiddle_kernel(double* tw) {
     else if (m < kTb4) { base = kTb3; P = 25; RAD = 5; }
     else if (m < kTb5) { base = kTb4; P = 125; RAD = 4; }
     else { base = kTb5; P = 500; RAD = 4; }
-    const int k = (m - base) / (RAD - 1), r = (m - base) % (RAD - 1) + 1;
+    const int k = (m - base) % P, r = (m - base) / P + 1;
     st[m] = tw32[r * k * (2 * kFFT / (P * RAD))];
 }
 
@@ -307,6 +308,11 @@ __device__ __forceinline__ f2 sub_mi(f2 a, f2 d) {  // a + i d = (a.x - d.y, a.y
     return r;
 }
 
+// LDS reads one wave-instruction per access: volatile keeps the compiler from pairing
+// them into ds_read2_b64, which costs 8 LDS cycles against 2 x 2 for two ds_read_b64
+typedef const volatile __attribute__((address_space(3))) f2* lds_f2p;
+__device__ __forceinline__ f2 ldsr(const f2* p) { return *(lds_f2p)(p); }
+
 // in-place radix-RAD Stockham stage (P = product of the previous radices, TB its
 // twiddle table base); WIN: stage 1 also detrends and Hann-windows the raw packed
 // samples it reads.  Every read is unconditional (the lanes of a partial last row
@@ -323,7 +329,7 @@ __device__ __forceinline__ void wstage(f2* z, const f2* Ts, const f2* __restrict
         const bool own = 64 * (q + 1) <= S || lane + 64 * q < S;
 #pragma unroll
         for (int r = 0; r < RAD; ++r) {
-            u[q][r] = z[i + r * S];
+            u[q][r] = ldsr(z + i + r * S);
             if constexpr (WIN) part += own ? u[q][r].x + u[q][r].y : 0.f;
         }
     }
@@ -351,9 +357,9 @@ __device__ __forceinline__ void wstage(f2* z, const f2* Ts, const f2* __restrict
         const bool own = 64 * (q + 1) <= S || lane + 64 * q < S;
         const int k = i % P;
         if constexpr (P > 1) {  // first stage: every twiddle is 1
-            const f2* tp = Ts + TB + k * (RAD - 1);
+            const f2* tp = Ts + TB + k;
 #pragma unroll
-            for (int r = 1; r < RAD; ++r) u[q][r] = cmulv(u[q][r], tp[r - 1]);
+            for (int r = 1; r < RAD; ++r) u[q][r] = cmulv(u[q][r], ldsr(tp + (r - 1) * P));
         }
         f2 U[RAD];
         if constexpr (RAD == 4) {
@@ -474,12 +480,12 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         for (int i = 0; i < kLaneBins; ++i) {
             const int k = l6 + 64 * i;
             if (64 * (i + 1) <= kBins || k < kBins) {
-                const f2 Zk = z[64 * (i + 1) <= kFFT ? k : (k == kFFT ? 0 : k)];
-                const f2 Zc = z[i > 0 ? kFFT - k : (k == 0 ? 0 : kFFT - k)];
+                const f2 Zk = ldsr(z + (64 * (i + 1) <= kFFT ? k : (k == kFFT ? 0 : k)));
+                const f2 Zc = ldsr(z + (i > 0 ? kFFT - k : (k == 0 ? 0 : kFFT - k)));
                 f2 sv, dv;
                 asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
                 asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
-                const f2 x = add_mi(sv, cmulv(dv, Tu[k]));
+                const f2 x = add_mi(sv, cmulv(dv, ldsr(Tu + k)));
                 acc[i] = fmaf(x.x, x.x, fmaf(x.y, x.y, acc[i]));
             }
             if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // (bounded live ranges: 4 bins at a time)
