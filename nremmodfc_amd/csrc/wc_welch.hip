@@ -251,9 +251,9 @@ constexpr int kWv = 4;       // waves (columns in flight) per simulation
 constexpr int kSimsWg = 2;   // simulations per workgroup
 constexpr int kLaneBins = (kBins + 63) / 64;  // 32
 #ifndef WC_WELCH_PF_EARLY
-#define WC_WELCH_PF_EARLY 10
+#define WC_WELCH_PF_EARLY 7
 #endif
-constexpr int kPfEarly = WC_WELCH_PF_EARLY;  // float4 of the next column fetched right after stage 1
+constexpr int kPfEarly = WC_WELCH_PF_EARLY;  // rows of the next column fetched right after stage 1
 // per-stage twiddle tables: entry (k, r) = T^(r k TS) at base + (r - 1) P + k (r-major: the
 // lanes of a row read consecutive k, conflict-free; r is an immediate offset)
 constexpr int kTb2 = 0, kTb3 = kTb2 + 5 * 4, kTb4 = kTb3 + 25 * 4, kTb5 = kTb4 + 125 * 3;
@@ -313,83 +313,152 @@ __device__ __forceinline__ f2 sub_mi(f2 a, f2 d) {  // a + i d = (a.x - d.y, a.y
 typedef const volatile __attribute__((address_space(3))) f2* lds_f2p;
 __device__ __forceinline__ f2 ldsr(const f2* p) { return *(lds_f2p)(p); }
 
-// in-place radix-RAD Stockham stage (P = product of the previous radices, TB its
-// twiddle table base); WIN: stage 1 also detrends and Hann-windows the raw packed
-// samples it reads.  Every read is unconditional (the lanes of a partial last row
+// Radix-RAD Stockham stage, in place (P = product of the previous radices, TB its
+// twiddle table base).  Every read is unconditional (the lanes of a partial last row
 // re-read the row's last butterfly, index clamped); only that row's writes are masked.
-template <int RAD, int P, int TB, bool WIN>
-__device__ __forceinline__ void wstage(f2* z, const f2* Ts, const f2* __restrict__ hann, int lane) {
-    constexpr int S = kFFT / RAD;
-    constexpr int NB = (S + 63) / 64;
-    f2 u[NB][RAD];
-    float part = 0.f;
-#pragma unroll
-    for (int q = 0; q < NB; ++q) {
-        const int i = 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1);
-        const bool own = 64 * (q + 1) <= S || lane + 64 * q < S;
-#pragma unroll
-        for (int r = 0; r < RAD; ++r) {
-            u[q][r] = ldsr(z + i + r * S);
-            if constexpr (WIN) part += own ? u[q][r].x + u[q][r].y : 0.f;
-        }
+template <int RAD, int P> struct Rows {
+    static constexpr int S = kFFT / RAD, NB = (S + 63) / 64;
+    __device__ static int idx(int lane, int q) { return 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1); }
+    __device__ static bool own(int lane, int q) { return 64 * (q + 1) <= S || lane + 64 * q < S; }
+};
+
+template <int RAD>
+__device__ __forceinline__ void butterfly(const f2 (&u)[RAD], f2 (&U)[RAD]) {
+    if constexpr (RAD == 4) {
+        const f2 a = u[0] + u[2], b = u[0] - u[2];
+        const f2 c = u[1] + u[3], d = u[1] - u[3];
+        U[0] = a + c;
+        U[2] = a - c;
+        U[1] = add_mi(b, d);  // b - i d
+        U[3] = sub_mi(b, d);  // b + i d
+    } else {
+        const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+        const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+        const f2 t1 = u[1] + u[4], t2 = u[2] + u[3];
+        const f2 t3 = u[1] - u[4], t4 = u[2] - u[3];
+        U[0] = u[0] + t1 + t2;
+        const f2 a1 = u[0] + c1 * t1 + c2 * t2;
+        const f2 a2 = u[0] + c2 * t1 + c1 * t2;
+        const f2 b1 = s1 * t3 + s2 * t4, b2 = s2 * t3 - s1 * t4;
+        U[1] = add_mi(a1, b1);  // a1 - i b1
+        U[4] = sub_mi(a1, b1);
+        U[2] = add_mi(a2, b2);
+        U[3] = sub_mi(a2, b2);
     }
-    if constexpr (WIN) {
-        // the first stage reads every raw sample: column mean (constant detrend), then
-        // the periodic Hann window w(t) = 0.5 - 0.5 cos(2 pi t / 4000) on the packed pairs
-        f2 hw[NB][RAD];
+}
+
+template <int RAD, int P>
+__device__ __forceinline__ void write_rows(f2* z, f2 (&u)[Rows<RAD, P>::NB][RAD], int lane) {
+    using R = Rows<RAD, P>;
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            const int i = 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1);
-#pragma unroll
-            for (int r = 0; r < RAD; ++r) hw[q][r] = hann[i + r * S];  // (w(2m), w(2m+1))
-        }
-        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-        const float mean = part / (float)kSeg;
-#pragma unroll
-        for (int q = 0; q < NB; ++q)
-#pragma unroll
-            for (int r = 0; r < RAD; ++r) u[q][r] = (u[q][r] - mean) * hw[q][r];
-    }
-    wave_sync();
-#pragma unroll
-    for (int q = 0; q < NB; ++q) {
-        const int i = 64 * (q + 1) <= S ? lane + 64 * q : min(lane + 64 * q, S - 1);
-        const bool own = 64 * (q + 1) <= S || lane + 64 * q < S;
-        const int k = i % P;
-        if constexpr (P > 1) {  // first stage: every twiddle is 1
-            const f2* tp = Ts + TB + k;
-#pragma unroll
-            for (int r = 1; r < RAD; ++r) u[q][r] = cmulv(u[q][r], ldsr(tp + (r - 1) * P));
-        }
+    for (int q = 0; q < R::NB; ++q) {
+        const int i = R::idx(lane, q), k = i % P;
         f2 U[RAD];
-        if constexpr (RAD == 4) {
-            const f2 a = u[q][0] + u[q][2], b = u[q][0] - u[q][2];
-            const f2 c = u[q][1] + u[q][3], d = u[q][1] - u[q][3];
-            U[0] = a + c;
-            U[2] = a - c;
-            U[1] = add_mi(b, d);  // b - i d
-            U[3] = sub_mi(b, d);  // b + i d
-        } else {
-            const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
-            const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
-            const f2 t1 = u[q][1] + u[q][4], t2 = u[q][2] + u[q][3];
-            const f2 t3 = u[q][1] - u[q][4], t4 = u[q][2] - u[q][3];
-            U[0] = u[q][0] + t1 + t2;
-            const f2 a1 = u[q][0] + c1 * t1 + c2 * t2;
-            const f2 a2 = u[q][0] + c2 * t1 + c1 * t2;
-            const f2 b1 = s1 * t3 + s2 * t4, b2 = s2 * t3 - s1 * t4;
-            U[1] = add_mi(a1, b1);  // a1 - i b1
-            U[4] = sub_mi(a1, b1);
-            U[2] = add_mi(a2, b2);
-            U[3] = sub_mi(a2, b2);
-        }
+        butterfly<RAD>(u[q], U);
         const int j = (i - k) * RAD + k;
-        if (own) {
+        if (R::own(lane, q)) {
 #pragma unroll
             for (int s2i = 0; s2i < RAD; ++s2i) z[j + s2i * P] = U[s2i];
         }
     }
+}
+
+// stage 1 (radix 5, no twiddles) fed from registers: x[q][r] = packed point i + 400 r of
+// the raw column; the column mean (constant detrend) and the periodic Hann window
+// w(t) = 0.5 - 0.5 cos(2 pi t / 4000) are applied on the way in
+__device__ __forceinline__ void wstage1(f2* z, f2 (&x)[7][5], const f2* __restrict__ hann, int lane) {
+    using R = Rows<5, 1>;
+    float part = 0.f;
+    f2 hw[7][5];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        const int i = R::idx(lane, q);
+#pragma unroll
+        for (int r = 0; r < 5; ++r) {
+            part += R::own(lane, q) ? x[q][r].x + x[q][r].y : 0.f;
+            hw[q][r] = hann[i + r * R::S];  // (w(2m), w(2m+1))
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    const float mean = part / (float)kSeg;
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+#pragma unroll
+        for (int r = 0; r < 5; ++r) x[q][r] = (x[q][r] - mean) * hw[q][r];
+    write_rows<5, 1>(z, x, lane);
     wave_sync();
+}
+
+template <int RAD, int P, int TB>
+__device__ __forceinline__ void wstage(f2* z, const f2* Ts, int lane) {
+    using R = Rows<RAD, P>;
+    f2 u[R::NB][RAD];
+#pragma unroll
+    for (int q = 0; q < R::NB; ++q) {
+        const int i = R::idx(lane, q);
+#pragma unroll
+        for (int r = 0; r < RAD; ++r) u[q][r] = ldsr(z + i + r * R::S);
+    }
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < R::NB; ++q) {
+        const f2* tp = Ts + TB + R::idx(lane, q) % P;
+#pragma unroll
+        for (int r = 1; r < RAD; ++r) u[q][r] = cmulv(u[q][r], ldsr(tp + (r - 1) * P));
+    }
+    write_rows<RAD, P>(z, u, lane);
+    wave_sync();
+}
+
+// Last stage (radix 4, P = 500) fused with the real-FFT unpack, all in registers.
+// Butterfly i produces Z_{i + 500 s}, s = 0..3; bin k pairs Z_k with Z_{2000-k}, and
+// Z_{2000 - (i + 500 s)} is slot 3 - s of butterfly 500 - i.  Rows 0..3 of a lane hold
+// butterflies m = lane + 64 q (m <= 250) and rows 4..7 their partners 500 - m, so every
+// pair meets in one lane: 2 X_k = s - i p and 2 X_{2000-k} = conj(s + i p), with
+// s = Z_k + conj Z_c, d = Z_k - conj Z_c, p = T^k d.  Butterflies 0 and 250 are their
+// own partners (Z_c = slot (4 - s) % 4 resp. 3 - s of the same row).
+// acc[q][s][0] collects bin m + 500 s, acc[q][s][1] bin 2000 - m - 500 s (times 4).
+__device__ __forceinline__ int last_row(int lane, int q) {
+    return q < 4 ? min(lane + 64 * q, 250) : 500 - min(max(lane + 64 * (q - 4), 1), 249);
+}
+__device__ __forceinline__ void wstage5_unpack(const f2* z, const f2* Ts, const f2* Tu, float (&acc)[4][4][2],
+                                               int lane) {
+    f2 u[8][4];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int i = last_row(lane, q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) u[q][r] = ldsr(z + i + 500 * r);
+    }
+    wave_sync();  // (the next column's stage 1 overwrites z)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int i = last_row(lane, q);
+#pragma unroll
+        for (int r = 1; r < 4; ++r) u[q][r] = cmulv(u[q][r], ldsr(Ts + kTb5 + (r - 1) * 500 + i));
+        f2 U[4];
+        butterfly<4>(u[q], U);
+#pragma unroll
+        for (int s2i = 0; s2i < 4; ++s2i) u[q][s2i] = U[s2i];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int m = last_row(lane, q);
+#pragma unroll
+        for (int s2i = 0; s2i < 4; ++s2i) {
+            const f2 Zk = u[q][s2i];
+            f2 Zc = u[q + 4][3 - s2i];
+            if (q == 0) Zc = m == 0 ? u[0][(4 - s2i) & 3] : Zc;
+            if (q == 3) Zc = m == 250 ? u[3][3 - s2i] : Zc;
+            f2 sv, dv;
+            asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
+            asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
+            const f2 pv = cmulv(dv, ldsr(Tu + m + 500 * s2i));
+            const f2 xa = add_mi(sv, pv), xb = sub_mi(sv, pv);
+            acc[q][s2i][0] = fmaf(xa.x, xa.x, fmaf(xa.y, xa.y, acc[q][s2i][0]));
+            acc[q][s2i][1] = fmaf(xb.x, xb.x, fmaf(xb.y, xb.y, acc[q][s2i][1]));
+        }
+    }
 }
 
 __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const WelchArgs a) {
@@ -399,49 +468,39 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
     const int b = blockIdx.x * kSimsWg + wg / kWv;        // this wave's simulation
     const int ncol = b < a.B ? a.N : 0;
     f2* z = reinterpret_cast<f2*>(smem) + wg * kFFT;
-    float* zf = reinterpret_cast<float*>(z);
     f2* Tu = reinterpret_cast<f2*>(smem) + kWv * kSimsWg * kFFT;  // T^k for the unpack
     f2* Ts = Tu + kUnpTw;                                          // per-stage tables
     const float* twg = reinterpret_cast<const float*>(a.tw + 2 * kSeg);  // fp32 tables: T, Hann, stage
     const f2* hann = reinterpret_cast<const f2*>(twg) + kSeg;
     const float* E = static_cast<const float*>(a.E);
-    float acc[kLaneBins];
+    float acc[4][4][2];
 #pragma unroll
-    for (int i = 0; i < kLaneBins; ++i) acc[i] = 0.f;
-    // ring runs of the segment (<= 5, wave-uniform): sample t of run r is at column offset ro[r] + t
-    int rt[5], ro[5];
-    {
-        int t = 0;
+    for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
-            rt[r] = t < kSeg ? t : kSeg + 1;
-            ro[r] = 0;
-            if (t < kSeg) {
-                const int64_t ts = a.seg0 + t;
-                const int64_t q = ts / a.slot, rr = ts % a.slot;
-                ro[r] = (int)((q % a.nslots) * a.slot + rr) - t;
-                t += (int)min((int64_t)(kSeg - t), a.slot - rr);
-            }
-        }
-    }
-    // the column's 4000 samples as 16 float4 per lane (t = 256 i + 4 lane; each lane's 16 B
-    // lie in one ring run); the next column is fetched into these registers while the
-    // current one is transformed (branch-free: lanes past the segment end re-read its last
-    // 16 B, and a wave's last column re-fetches itself, an L2 hit)
-    typedef float f4v __attribute__((ext_vector_type(4)));  // (native vector: HIP's float4 struct copies stay in scratch)
-    f4v pf[16];
+        for (int s2i = 0; s2i < 4; ++s2i) acc[q][s2i][0] = acc[q][s2i][1] = 0.f;
+    // the ring is circular per column: sample seg0 + t sits at (seg0 + t) mod L, L = slot * nslots
+    const unsigned L = (unsigned)(a.slot * a.nslots);
+    const unsigned base = (unsigned)(a.seg0 % L);
+    // stage-1 inputs come straight from HBM into registers, in the butterfly layout
+    // (x[q][r] = packed point i + 400 r, i = lane + 64 q); the next column is fetched
+    // while the current one is transformed (branch-free: the clamped lanes of row 6
+    // re-read a valid point, and a wave's last column re-fetches itself, an L2 hit)
+    f2 x[7][5];
     const int64_t bc = (int64_t)min(b, a.B - 1) * a.N;
-#define WELCH_FETCH(n, I0, I1)                                                                 \
+    // (uniform column base + 32-bit unsigned lane offset: the saddr form of global_load)
+#define WELCH_FETCH(n, Q0, Q1, LN)                                                             \
     {                                                                                          \
         const float* col_ = E + (bc + (n)) * a.ld;                                             \
-        _Pragma("unroll") for (int i = I0; i < I1; ++i) {                                      \
-            const int t = min(256 * i + 4 * lane, kSeg - 4);                                   \
-            int off = ro[0] + t;                                                               \
-            _Pragma("unroll") for (int r = 1; r < 5; ++r) off = t >= rt[r] ? ro[r] + t : off;  \
-            pf[i] = *reinterpret_cast<const f4v*>(col_ + off);                                 \
+        _Pragma("unroll") for (int q = Q0; q < Q1; ++q) {                                      \
+            const int i_ = Rows<5, 1>::idx(LN, q);                                            \
+            _Pragma("unroll") for (int r = 0; r < 5; ++r) {                                    \
+                unsigned o_ = base + 2 * (i_ + 400 * r);                                       \
+                o_ = min(o_, o_ - L);                                                          \
+                x[q][r] = *reinterpret_cast<const f2*>(col_ + o_);                             \
+            }                                                                                  \
         }                                                                                      \
     }
-    WELCH_FETCH(min(w, a.N - 1), 0, 16);
+    WELCH_FETCH(min(w, a.N - 1), 0, 7, lane);
     {  // twiddle tables into LDS: T^0..T^2000 and the stage tables (the pad entry is never read)
         const f2* src = reinterpret_cast<const f2*>(twg);
         const f2* sst = reinterpret_cast<const f2*>(twg) + kSeg + kFFT;
@@ -451,55 +510,39 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
     __syncthreads();
 
     for (int n = w; n < ncol; n += kWv) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int t = 256 * i + 4 * lane;
-            if (256 * (i + 1) <= kSeg || t < kSeg) *reinterpret_cast<f4v*>(zf + t) = pf[i];
-        }
-        wave_sync();
-        // ---- Stockham 2000 = 5 * 5 * 5 * 4 * 4, window fused into the first stage ----
         // (the lane id is laundered per column so the compiler does not hoist hundreds
         // of loop-invariant twiddle offsets out of the column loop)
         int ln = lane;
         asm volatile("" : "+v"(ln));
         ln &= 63;  // (range-known again: unsigned index arithmetic, static masks)
-        wstage<5, 1, 0, true>(z, Ts, hann, ln);
+        // ---- Stockham 2000 = 5 * 5 * 5 * 4 * 4, window fused into the first stage,
+        //      the real-FFT unpack into the last ----
+        wstage1(z, x, hann, ln);
         // the Hann loads have retired: the next column's loads are the only VMEM in flight
         const int nn = n + kWv < ncol ? n + kWv : n;
-        WELCH_FETCH(nn, 0, kPfEarly);
-        wstage<5, 5, kTb2, false>(z, Ts, hann, ln);
-        wstage<5, 25, kTb3, false>(z, Ts, hann, ln);
-        wstage<4, 125, kTb4, false>(z, Ts, hann, ln);
-        wstage<4, 500, kTb5, false>(z, Ts, hann, ln);
-        WELCH_FETCH(nn, kPfEarly, 16);  // (the rest of the next column: fewer live registers through the stages)
-        // ---- unpack X_k = (Z_k + conj Z_-k)/2 - i/2 W^k (Z_k - conj Z_-k), |X_k|^2 ----
-        //      2 X_k = s - i W^k d with s = Z_k + conj Z_-k, d = Z_k - conj Z_-k; the 1/4 of
-        //      |X_k|^2 = |2 X_k|^2 / 4 is applied once, in the final fp64 combine (exact)
-        const int l6 = ln;
-#pragma unroll
-        for (int i = 0; i < kLaneBins; ++i) {
-            const int k = l6 + 64 * i;
-            if (64 * (i + 1) <= kBins || k < kBins) {
-                const f2 Zk = ldsr(z + (64 * (i + 1) <= kFFT ? k : (k == kFFT ? 0 : k)));
-                const f2 Zc = ldsr(z + (i > 0 ? kFFT - k : (k == 0 ? 0 : kFFT - k)));
-                f2 sv, dv;
-                asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
-                asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
-                const f2 x = add_mi(sv, cmulv(dv, ldsr(Tu + k)));
-                acc[i] = fmaf(x.x, x.x, fmaf(x.y, x.y, acc[i]));
-            }
-            if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // (bounded live ranges: 4 bins at a time)
-        }
-        wave_sync();  // the next column overwrites z
+        WELCH_FETCH(nn, 0, kPfEarly, ln);
+        wstage<5, 5, kTb2>(z, Ts, ln);
+        wstage<5, 25, kTb3>(z, Ts, ln);
+        wstage<4, 125, kTb4>(z, Ts, ln);
+        WELCH_FETCH(nn, kPfEarly, 7, ln);  // (the rest of the next column: fewer live registers through the stages)
+        wstage5_unpack(z, Ts, Tu, acc, ln);
     }
 #undef WELCH_FETCH
     // ---- combine each simulation's four waves (fp64) into its accumulator row (single writer) ----
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [kSimsWg][kWv][kBins]
 #pragma unroll
-    for (int i = 0; i < kLaneBins; ++i) {
-        const int k = lane + 64 * i;
-        if (k < kBins) red[wg * kBins + k] = acc[i];
+    for (int q = 0; q < 4; ++q) {
+        const int m = lane + 64 * q;
+#pragma unroll
+        for (int s2i = 0; s2i < 4; ++s2i) {
+            // each bin once: rows past m = 250 hold nothing; butterflies 0 and 250 pair
+            // with themselves, so their later slots repeat earlier bins
+            const bool ok = m <= 250 && !(m == 250 && s2i >= 2) && !(m == 0 && s2i == 3);
+            const int k = m + 500 * s2i;
+            if (ok) red[wg * kBins + k] = acc[q][s2i][0];
+            if (ok && !(m == 0 && s2i == 2)) red[wg * kBins + kFFT - k] = acc[q][s2i][1];
+        }
     }
     __syncthreads();
     for (int idx = threadIdx.x; idx < kSimsWg * kBins; idx += kWv * kSimsWg * 64) {

@@ -139,6 +139,33 @@ def test_welch_vs_oracle(cuda, dtype):
         assert peak[b].item() == osg.welch_peak(Eh[:, b, :])
 
 
+@pytest.mark.parametrize("B,N", [(5, 1), (2, 3), (4, 9)])
+def test_welch_f32_ring_wrap_and_small_n(cuda, B, N):
+    """fp32 product kernel: a segment that wraps the 4-slot ring (ld padded past
+    slot * nslots) gives the same accumulator bits as the same samples read from a
+    contiguous column; N < 4 leaves waves idle; odd B leaves half a workgroup empty.
+    Each simulation's PSD also matches the oracle."""
+    T = 6000
+    X = torch.from_numpy(_e_like(T, B * N, B * 10 + N).T.copy()).to("cuda", torch.float32)  # [C][T]
+    slot, nslots, ld = 1000, 4, 4096
+    ring = torch.zeros((B * N, ld), dtype=torch.float32, device="cuda")
+    for t0 in range(2000, T, slot):  # samples [2000, 6000) into slots (t // slot) % 4
+        q = (t0 // slot) % nslots
+        ring[:, q * slot:(q + 1) * slot] = X[:, t0:t0 + slot]
+    a = wsg.WelchAccumulator(B, N)
+    a.accumulate(ring.reshape(-1), ld, slot, nslots, 2000)  # runs: slots 2, 3, 0, 1
+    c = wsg.WelchAccumulator(B, N)
+    c.accumulate(X.reshape(-1), T, T, 1, 2000)
+    torch.cuda.synchronize()
+    assert torch.equal(a.acc, c.acc)
+    _, psd = a.peak(want_psd=True)
+    Xh = X.double().cpu().numpy().reshape(B, N, T)
+    for b in range(B):
+        f, P = osg.welch_psd(Xh[b][:, 2000:], 500.0, 4000)
+        mp = P.mean(axis=0)
+        np.testing.assert_allclose(psd[b].cpu().numpy(), mp, rtol=2e-4, atol=2e-4 * mp.max())
+
+
 def test_welch_golden_full_length(cuda):
     """300,000-sample input of the SciPy golden: node-mean PSD and peak."""
     inp = inputs()
