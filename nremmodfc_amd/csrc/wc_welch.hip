@@ -256,8 +256,9 @@ constexpr int kLaneBins = (kBins + 63) / 64;  // 32
 constexpr int kPfEarly = WC_WELCH_PF_EARLY;  // rows of the next column fetched right after stage 1
 // per-stage twiddle tables: entry (k, r) = T^(r k TS) at base + (r - 1) P + k (r-major: the
 // lanes of a row read consecutive k, conflict-free; r is an immediate offset)
-constexpr int kTb2 = 0, kTb3 = kTb2 + 5 * 4, kTb4 = kTb3 + 25 * 4, kTb5 = kTb4 + 125 * 3;
-constexpr int kStageTw = kTb5 + 500 * 3;  // 1995
+// (stages 5 x 5 x 5 x 16; the first has no twiddles)
+constexpr int kTb2 = 0, kTb3 = kTb2 + 5 * 4, kTb4 = kTb3 + 25 * 4;
+constexpr int kStageTw = kTb4 + 125 * 15;  // 1995
 constexpr int kUnpTw = kBins + 1;         // T^k, k in [0, 2000] (+1 pad: 16-B aligned stage tables)
 constexpr size_t kWelchLds = (size_t)kWv * kSimsWg * kFFT * 8 + (size_t)(kUnpTw + kStageTw) * 8;  // 159,976 B
 
@@ -273,8 +274,7 @@ __global__ void stage_twiddle_kernel(double* tw) {
     int base, P, RAD;
     if (m < kTb3) { base = kTb2; P = 5; RAD = 5; }
     else if (m < kTb4) { base = kTb3; P = 25; RAD = 5; }
-    else if (m < kTb5) { base = kTb4; P = 125; RAD = 4; }
-    else { base = kTb5; P = 500; RAD = 4; }
+    else { base = kTb4; P = 125; RAD = 16; }
     const int k = (m - base) % P, r = (m - base) / P + 1;
     st[m] = tw32[r * k * (2 * kFFT / (P * RAD))];
 }
@@ -410,54 +410,71 @@ __device__ __forceinline__ void wstage(f2* z, const f2* Ts, int lane) {
     wave_sync();
 }
 
-// Last stage (radix 4, P = 500) fused with the real-FFT unpack, all in registers.
-// Butterfly i produces Z_{i + 500 s}, s = 0..3; bin k pairs Z_k with Z_{2000-k}, and
-// Z_{2000 - (i + 500 s)} is slot 3 - s of butterfly 500 - i.  Rows 0..3 of a lane hold
-// butterflies m = lane + 64 q (m <= 250) and rows 4..7 their partners 500 - m, so every
-// pair meets in one lane: 2 X_k = s - i p and 2 X_{2000-k} = conj(s + i p), with
-// s = Z_k + conj Z_c, d = Z_k - conj Z_c, p = T^k d.  Butterflies 0 and 250 are their
-// own partners (Z_c = slot (4 - s) % 4 resp. 3 - s of the same row).
-// acc[q][s][0] collects bin m + 500 s, acc[q][s][1] bin 2000 - m - 500 s (times 4).
-__device__ __forceinline__ int last_row(int lane, int q) {
-    return q < 4 ? min(lane + 64 * q, 250) : 500 - min(max(lane + 64 * (q - 4), 1), 249);
-}
-__device__ __forceinline__ void wstage5_unpack(const f2* z, const f2* Ts, const f2* Tu, float (&acc)[4][4][2],
-                                               int lane) {
-    f2 u[8][4];
+// 16-point DFT U[s] = sum_r u[r] W16^(r s) as 4 x 4 (r = 4 r1 + r2, s = s1 + 4 s2):
+// radix-4 over r1, twiddle W16^(r2 s1), radix-4 over r2
+__device__ __forceinline__ void dft16(f2 (&u)[16]) {
+    constexpr float h = 0.70710678118654752440f, c = 0.92387953251128675613f, d = 0.38268343236508977173f;
+    f2 v[4][4];  // v[r2][s1]
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int i = last_row(lane, q);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) u[q][r] = ldsr(z + i + 500 * r);
+    for (int r2 = 0; r2 < 4; ++r2) {
+        const f2 in[4] = {u[r2], u[4 + r2], u[8 + r2], u[12 + r2]};
+        butterfly<4>(in, v[r2]);
     }
+    // W16^j = (cos, -sin)(2 pi j / 16): j = r2 s1 in {1, 2, 3, 4, 6, 9}
+    v[1][1] = cmulv(v[1][1], (f2){c, -d});
+    v[1][2] = cmulv(v[1][2], (f2){h, -h});
+    v[1][3] = cmulv(v[1][3], (f2){d, -c});
+    v[2][1] = cmulv(v[2][1], (f2){h, -h});
+    v[2][2] = cmulv(v[2][2], (f2){0.f, -1.f});
+    v[2][3] = cmulv(v[2][3], (f2){-h, -h});
+    v[3][1] = cmulv(v[3][1], (f2){d, -c});
+    v[3][2] = cmulv(v[3][2], (f2){-h, -h});
+    v[3][3] = cmulv(v[3][3], (f2){-c, d});
+#pragma unroll
+    for (int s1 = 0; s1 < 4; ++s1) {
+        const f2 in[4] = {v[0][s1], v[1][s1], v[2][s1], v[3][s1]};
+        f2 o[4];
+        butterfly<4>(in, o);
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) u[s1 + 4 * s2] = o[s2];
+    }
+}
+
+// Last stage (radix 16, P = 125) fused with the real-FFT unpack, all in registers.
+// Butterfly i produces Z_{i + 125 s}, s = 0..15; bin k pairs Z_k with Z_{2000-k}, and
+// Z_{2000 - (i + 125 s)} is slot 15 - s of butterfly 125 - i.  Row 0 of a lane holds
+// butterfly m = lane (m <= 62) and row 1 its partner 125 - m, so every pair meets in
+// one lane: 2 X_k = s - i p and 2 X_{2000-k} = conj(s + i p), with s = Z_k + conj Z_c,
+// d = Z_k - conj Z_c, p = T^k d.  Butterfly 0 is its own partner (Z_c = slot
+// (16 - s) % 16 of the same row).  acc[s][0] collects bin m + 125 s, acc[s][1] bin
+// 2000 - m - 125 s (times 4).
+__device__ __forceinline__ void wstage_last_unpack(const f2* z, const f2* Ts, const f2* Tu, float (&acc)[16][2],
+                                                   int lane) {
+    const int m = min(lane, 62);
+    const int rows[2] = {m, 125 - max(m, 1)};
+    f2 u[2][16];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) u[q][r] = ldsr(z + rows[q] + 125 * r);
     wave_sync();  // (the next column's stage 1 overwrites z)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int i = last_row(lane, q);
+    for (int q = 0; q < 2; ++q) {
 #pragma unroll
-        for (int r = 1; r < 4; ++r) u[q][r] = cmulv(u[q][r], ldsr(Ts + kTb5 + (r - 1) * 500 + i));
-        f2 U[4];
-        butterfly<4>(u[q], U);
-#pragma unroll
-        for (int s2i = 0; s2i < 4; ++s2i) u[q][s2i] = U[s2i];
+        for (int r = 1; r < 16; ++r) u[q][r] = cmulv(u[q][r], ldsr(Ts + kTb4 + (r - 1) * 125 + rows[q]));
+        dft16(u[q]);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int m = last_row(lane, q);
-#pragma unroll
-        for (int s2i = 0; s2i < 4; ++s2i) {
-            const f2 Zk = u[q][s2i];
-            f2 Zc = u[q + 4][3 - s2i];
-            if (q == 0) Zc = m == 0 ? u[0][(4 - s2i) & 3] : Zc;
-            if (q == 3) Zc = m == 250 ? u[3][3 - s2i] : Zc;
-            f2 sv, dv;
-            asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
-            asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
-            const f2 pv = cmulv(dv, ldsr(Tu + m + 500 * s2i));
-            const f2 xa = add_mi(sv, pv), xb = sub_mi(sv, pv);
-            acc[q][s2i][0] = fmaf(xa.x, xa.x, fmaf(xa.y, xa.y, acc[q][s2i][0]));
-            acc[q][s2i][1] = fmaf(xb.x, xb.x, fmaf(xb.y, xb.y, acc[q][s2i][1]));
-        }
+    for (int s2i = 0; s2i < 16; ++s2i) {
+        const f2 Zk = u[0][s2i];
+        const f2 Zc = m == 0 ? u[0][(16 - s2i) & 15] : u[1][15 - s2i];
+        f2 sv, dv;
+        asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
+        asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
+        const f2 pv = cmulv(dv, ldsr(Tu + m + 125 * s2i));
+        const f2 xa = add_mi(sv, pv), xb = sub_mi(sv, pv);
+        acc[s2i][0] = fmaf(xa.x, xa.x, fmaf(xa.y, xa.y, acc[s2i][0]));
+        acc[s2i][1] = fmaf(xb.x, xb.x, fmaf(xb.y, xb.y, acc[s2i][1]));
     }
 }
 
@@ -473,11 +490,9 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
     const float* twg = reinterpret_cast<const float*>(a.tw + 2 * kSeg);  // fp32 tables: T, Hann, stage
     const f2* hann = reinterpret_cast<const f2*>(twg) + kSeg;
     const float* E = static_cast<const float*>(a.E);
-    float acc[4][4][2];
+    float acc[16][2];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int s2i = 0; s2i < 4; ++s2i) acc[q][s2i][0] = acc[q][s2i][1] = 0.f;
+    for (int s2i = 0; s2i < 16; ++s2i) acc[s2i][0] = acc[s2i][1] = 0.f;
     // the ring is circular per column: sample seg0 + t sits at (seg0 + t) mod L, L = slot * nslots
     const unsigned L = (unsigned)(a.slot * a.nslots);
     const unsigned base = (unsigned)(a.seg0 % L);
@@ -515,7 +530,7 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         int ln = lane;
         asm volatile("" : "+v"(ln));
         ln &= 63;  // (range-known again: unsigned index arithmetic, static masks)
-        // ---- Stockham 2000 = 5 * 5 * 5 * 4 * 4, window fused into the first stage,
+        // ---- Stockham 2000 = 5 * 5 * 5 * 16, window fused into the first stage,
         //      the real-FFT unpack into the last ----
         wstage1(z, x, hann, ln);
         // the Hann loads have retired: the next column's loads are the only VMEM in flight
@@ -523,26 +538,21 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         WELCH_FETCH(nn, 0, kPfEarly, ln);
         wstage<5, 5, kTb2>(z, Ts, ln);
         wstage<5, 25, kTb3>(z, Ts, ln);
-        wstage<4, 125, kTb4>(z, Ts, ln);
         WELCH_FETCH(nn, kPfEarly, 7, ln);  // (the rest of the next column: fewer live registers through the stages)
-        wstage5_unpack(z, Ts, Tu, acc, ln);
+        wstage_last_unpack(z, Ts, Tu, acc, ln);
     }
 #undef WELCH_FETCH
     // ---- combine each simulation's four waves (fp64) into its accumulator row (single writer) ----
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [kSimsWg][kWv][kBins]
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int m = lane + 64 * q;
-#pragma unroll
-        for (int s2i = 0; s2i < 4; ++s2i) {
-            // each bin once: rows past m = 250 hold nothing; butterflies 0 and 250 pair
-            // with themselves, so their later slots repeat earlier bins
-            const bool ok = m <= 250 && !(m == 250 && s2i >= 2) && !(m == 0 && s2i == 3);
-            const int k = m + 500 * s2i;
-            if (ok) red[wg * kBins + k] = acc[q][s2i][0];
-            if (ok && !(m == 0 && s2i == 2)) red[wg * kBins + kFFT - k] = acc[q][s2i][1];
-        }
+    for (int s2i = 0; s2i < 16; ++s2i) {
+        // each bin once: lane 63 repeats lane 62; butterfly 0 pairs with itself, so its
+        // slots past 8 repeat earlier bins and slot 8 is bin 1000 twice
+        const bool ok = lane < 63 && !(lane == 0 && s2i > 8);
+        const int k = lane + 125 * s2i;
+        if (ok) red[wg * kBins + k] = acc[s2i][0];
+        if (ok && !(lane == 0 && s2i == 8)) red[wg * kBins + kFFT - k] = acc[s2i][1];
     }
     __syncthreads();
     for (int idx = threadIdx.x; idx < kSimsWg * kBins; idx += kWv * kSimsWg * 64) {
