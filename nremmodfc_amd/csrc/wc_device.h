@@ -16,6 +16,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 // ---------------- noise: Philox4x32-10 (must match oracle/wc_oracle.c) ----------------
 // key = (WC_PHILOX_KEY0, WC_PHILOX_KEY1) for every simulation (wave-uniform: the
@@ -157,6 +159,24 @@ __device__ __forceinline__ void split3(const float v[4], bf16x4& hi, bf16x4& mid
         hi[2 * p + 1] = h[1];
         mid[2 * p] = m[0];
         mid[2 * p + 1] = m[1];
+        lo[2 * p] = l[0];
+        lo[2 * p + 1] = l[1];
+    }
+}
+
+// fp16 two-part split of v * 2^10 (v in [0, 1]): hi = fp16(RNE), lo = fp16(v 2^10 - hi);
+// v 2^10 - hi is exact in fp32, so hi + lo carries 22 significant bits and, scaled,
+// both parts stay normal fp16 down to v ~ 1e-4
+__device__ __forceinline__ void split2h(const float v[4], f16x4& hi, f16x4& lo) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const f2 x = (f2){v[2 * p], v[2 * p + 1]} * 1024.0f;
+        const h2 h = __builtin_convertvector(x, h2);
+        const h2 l = __builtin_convertvector(x - __builtin_convertvector(h, f2), h2);
+        hi[2 * p] = h[0];
+        hi[2 * p + 1] = h[1];
         lo[2 * p] = l[0];
         lo[2 * p + 1] = l[1];
     }

@@ -15,10 +15,12 @@
 // streams the whole E vector back from LDS as MFMA B operands.
 //
 // Coupling arithmetic:
-//   fp32 product path (V_BF16X6): E and CM are split into three bf16 parts
-//     (hi + mid + lo, |x - sum| <= 2^-27 |x|) and the six cross terms of weight
-//     >= 2^-18 run on v_mfma_f32_16x16x32_bf16 with fp32 accumulation -- fp32-
-//     equivalent accuracy at 2.7x the rate of v_mfma_f32_16x16x4_f32.
+//   fp32 product path (V_F16X3): E 2^10 and CM sA (sA a power of two putting
+//     max|CM| just under 2^14) are split into two fp16 parts (hi + lo, 22
+//     significant bits, both normal over the range that matters) and the three
+//     cross terms hi.hi, hi.lo, lo.hi run on v_mfma_f32_16x16x32_f16 with fp32
+//     accumulation; 1/(2^10 sA) is folded into G.  Same trajectories vs the oracle
+//     as the six-term bf16 split (V_BF16X6, kept as an ablation) at half the MFMAs.
 //   fp64 parity path: v_mfma_f64_16x16x4_f64 (rows permuted, Tr<double>).
 // The elementwise update (two logistic sigmoids, homeostatic plasticity,
 // Philox4x32-10 noise + Box-Muller) runs on the VALU beside the MFMAs.
@@ -110,6 +112,57 @@ __global__ void build_frag_bf16(const double* __restrict__ sc, int N, bf16x8* __
     for (int p = 0; p < 3; ++p) frag[(size_t)(tc * 3 + p) * 64 + lane] = part[p];
 }
 
+// the two scale floats follow the fp16 image (inside the fp32 workspace, which is
+// sized for the 3-part bf16 image)
+__host__ __device__ constexpr size_t hf_scale_offset(int NT) { return (size_t)NT * (NT / 2) * 2 * 64 * 16 / 4; }
+
+// fp16 x3 coupling: CM scaled by sA = 2^(13 - e), max|CM| in [2^(e-1), 2^e), so every
+// |CM sA| < 2^14 (fp16 max 65504 with the 2^10-scaled E: products < 2^24).
+// scl[0] = sA, scl[1] = 1 / (2^10 sA) (folded into G by the kernel)
+__global__ void coupling_scale_kernel(const double* __restrict__ sc, int N, float* __restrict__ scl) {
+    __shared__ double red[256];
+    double m = 0.0;
+    for (int i = threadIdx.x; i < N * N; i += 256) m = fmax(m, fabs(sc[i]));
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int e = 0;
+        if (red[0] > 0.0) frexp(red[0], &e);
+        e = max(-100, min(100, e));
+        scl[0] = ldexpf(1.0f, 13 - e);
+        scl[1] = ldexpf(1.0f, e - 23);
+    }
+}
+
+// fp16 x3: frag[((T*NC + c)*2 + p)*64 + lane][jj] = part p of CM[..] sA, hi = fp16(x),
+// lo = fp16(x - hi) (same element order as build_frag_bf16)
+template <int NT>
+__global__ void build_frag_f16(const double* __restrict__ sc, int N, const float* __restrict__ scl,
+                               f16x8* __restrict__ frag) {
+    constexpr int NC = NT / 2;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= NT * NC * 64) return;
+    const int lane = idx & 63, tc = idx >> 6;
+    const int T = tc / NC, c = tc % NC;
+    const double sA = scl[0];
+    const int row = 16 * T + (lane & 15);
+    f16x8 part[2];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        const int col = 16 * (2 * c + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);
+        const double x = (row < N && col < N) ? sc[(size_t)row * N + col] * sA : 0.0;
+        const _Float16 h = (_Float16)(float)x;
+        part[0][jj] = h;
+        part[1][jj] = (_Float16)(float)(x - (double)(float)h);
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) frag[(size_t)(tc * 2 + p) * 64 + lane] = part[p];
+}
+
 // ---------------- variants ----------------
 enum : int {
     V_FRAG_REGS = 1,  // A-operand fragments held in registers (else streamed from LDS each step)
@@ -120,6 +173,7 @@ enum : int {
     V_BF16X3 = 64,    // ablation: only the three leading terms (~2^-17 relative)
     V_REC2 = 128,     // node-major E records buffered 2 deep: one 8-B store per node per 2 records
     V_REC4 = 256,     // ... 4 deep: one 16-B store per node per 4 records (host checks eligibility)
+    V_F16X3 = 512,    // fp32 coupling as three fp16 cross terms of two-part (22-bit) operands
 };
 
 // SG > 1: one workgroup holds SG groups of 16 simulations (SG x NW waves) that
@@ -130,11 +184,13 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     typedef __attribute__((ext_vector_type(4))) Real real4;
     static_assert(NT % NW == 0, "NW must divide NT");
     constexpr int OT = NT / NW;
-    constexpr int kTerms = (VAR & V_BF16X6) ? 6 : (VAR & V_BF16X3) ? 3 : 0;
-    constexpr bool kBf = kTerms > 0;
-    static_assert(!kBf || (sizeof(Real) == 4 && NT % 2 == 0), "bf16 coupling: fp32, even tile count");
-    constexpr int NC = NT / 2;  // bf16 k-chunks (2 tiles = 32 nodes)
+    constexpr bool kHf = (VAR & V_F16X3) != 0;
+    constexpr int kTerms = (VAR & V_BF16X6) ? 6 : (VAR & V_BF16X3) ? 3 : kHf ? 3 : 0;
+    constexpr bool kBf = kTerms > 0;  // 16-bit split coupling (bf16 or fp16 parts)
+    static_assert(!kBf || (sizeof(Real) == 4 && NT % 2 == 0), "split coupling: fp32, even tile count");
+    constexpr int NC = NT / 2;  // 16-bit k-chunks (2 tiles = 32 nodes)
     constexpr int NP = kTerms == 6 ? 3 : 2;
+    constexpr int PS = kHf ? 2 : 3;  // parts per chunk in the images
     constexpr bool kFragRegs = (VAR & V_FRAG_REGS) != 0;
     constexpr bool kRng = (VAR & V_NO_RNG) == 0;
     constexpr bool kMfma = (VAR & V_NO_MFMA) == 0;
@@ -142,14 +198,14 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr bool kParamRegs = sizeof(Real) == 4;  // fp64 re-reads G/sigmaE (register budget)
     // fp32 with the compensated a_ie: the folded-constant update (Sl holds -sigmaE log2 e)
     constexpr bool kFast = sizeof(Real) == 4 && kPairA;
-    constexpr int kFragUnits = kBf ? NT * NC * 3 : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
+    constexpr int kFragUnits = kBf ? NT * NC * PS : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     // LDS: [A-operand image, unless kFragRegs] [E exchange, 2 buffers, if NW > 1]
     const size_t frag_bytes = kFragRegs ? 0 : (size_t)kFragUnits * 64 * (kBf ? 16 : sizeof(real4));
     const int grp = SG == 1 ? 0 : (threadIdx.x >> 6) / NW;
     char* xraw = smem + frag_bytes;
-    bf16x8* xb16 = reinterpret_cast<bf16x8*>(xraw) + grp * (2 * NC * 3 * 64);  // [2][NC][3][64] per group
+    bf16x8* xb16 = reinterpret_cast<bf16x8*>(xraw) + grp * (2 * NC * PS * 64);  // [2][NC][PS][64] per group
     real4* xbn = reinterpret_cast<real4*>(xraw) + grp * (2 * NT * 64);         // [2][NT][64] per group
 
     const int lane = threadIdx.x & 63;
@@ -174,7 +230,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
 #pragma unroll
-                    for (int p = 0; p < NP; ++p) F16[u][c][p] = g16[(((T0 + u) * NC + c) * 3 + p) * 64 + lane];
+                    for (int p = 0; p < NP; ++p) F16[u][c][p] = g16[(((T0 + u) * NC + c) * PS + p) * 64 + lane];
         } else if constexpr (kRegN) {
 #pragma unroll
             for (int u = 0; u < OT; ++u)
@@ -190,6 +246,9 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     }
 
     const uint64_t key = a.keys[bb];
+    // fp16 coupling: the MFMA sums CM sA x E 2^10; 1 / (2^10 sA) is folded into G (exact)
+    Real gscale = 1;
+    if constexpr (kHf) gscale = reinterpret_cast<const float*>(a.frag)[hf_scale_offset(NT) + 1];
 
     // ---- own state and per-node parameters ----
     constexpr int PT = kParamRegs ? OT : 1;
@@ -206,7 +265,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             I[u][r] = ok ? (Real)a.I[o] : (Real)0;
             A[u][r].set(ok ? a.A[o] : 0.0);
             if constexpr (kParamRegs) {
-                Gc[u][r] = ok ? (Real)a.G[o] : (Real)0;
+                Gc[u][r] = ok ? (Real)a.G[o] * gscale : (Real)0;
                 Sl[u][r] = ok ? (kFast ? -1 : 1) * Tr<Real>::slope(a.sigmaE[o]) : (Real)0;
             }
         }
@@ -223,8 +282,13 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     bf16x4 h0, m0, l0, h1, m1, l1;
-                    split3(E[2 * c], h0, m0, l0);
-                    split3(E[2 * c + 1], h1, m1, l1);
+                    if constexpr (kHf) {
+                        split2h(E[2 * c], reinterpret_cast<f16x4&>(h0), reinterpret_cast<f16x4&>(m0));
+                        split2h(E[2 * c + 1], reinterpret_cast<f16x4&>(h1), reinterpret_cast<f16x4&>(m1));
+                    } else {
+                        split3(E[2 * c], h0, m0, l0);
+                        split3(E[2 * c + 1], h1, m1, l1);
+                    }
                     XB[c][0] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
                     XB[c][1] = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
                     if constexpr (NP == 3) XB[c][2] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -237,14 +301,15 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             }
         } else {
             if constexpr (kBf) {
-                bf16x4* x4 = reinterpret_cast<bf16x4*>(xb16 + buf * NC * 3 * 64);
+                bf16x4* x4 = reinterpret_cast<bf16x4*>(xb16 + buf * NC * PS * 64);
 #pragma unroll
                 for (int u = 0; u < OT; ++u) {
                     const int t = T0 + u;  // chunk t/2, half t&1 (runtime: address arithmetic only)
                     bf16x4 hmo[3];
-                    split3(E[u], hmo[0], hmo[1], hmo[2]);
+                    if constexpr (kHf) split2h(E[u], reinterpret_cast<f16x4&>(hmo[0]), reinterpret_cast<f16x4&>(hmo[1]));
+                    else split3(E[u], hmo[0], hmo[1], hmo[2]);
 #pragma unroll
-                    for (int p = 0; p < NP; ++p) x4[(((t >> 1) * 3 + p) * 64 + lane) * 2 + (t & 1)] = hmo[p];
+                    for (int p = 0; p < NP; ++p) x4[(((t >> 1) * PS + p) * 64 + lane) * 2 + (t & 1)] = hmo[p];
                 }
             } else {
                 real4* xb = xbn + buf * NT * 64;
@@ -342,14 +407,14 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         if constexpr (!kFragRegs || NW > 1) asm volatile("" : "+v"(fl));  // opaque: LDS reads stay in the loop
         if constexpr (kMfma && kBf) {
             const bf16x8* l16 = reinterpret_cast<const bf16x8*>(smem);
-            const bf16x8* xb = xb16 + buf * NC * 3 * 64;
+            const bf16x8* xb = xb16 + buf * NC * PS * 64;
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
                 bf16x8 xe[NP];
 #pragma unroll
                 for (int p = 0; p < NP; ++p) {
                     if constexpr (NW == 1) xe[p] = XB[c][p];
-                    else xe[p] = xb[(c * 3 + p) * 64 + fl];
+                    else xe[p] = xb[(c * PS + p) * 64 + fl];
                 }
 #pragma unroll
                 for (int u = 0; u < OT; ++u) {
@@ -357,7 +422,14 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                     for (int p = 0; p < NP; ++p) {
                         if constexpr (kFragRegs) f[p] = F16[u][c][p];
-                        else f[p] = l16[(((T0 + u) * NC + c) * 3 + p) * 64 + fl];
+                        else f[p] = l16[(((T0 + u) * NC + c) * PS + p) * 64 + fl];
+                    }
+                    if constexpr (kHf) {  // small terms first: 2^-11 (lo.hi, hi.lo), 1 (hi.hi)
+                        typedef f16x8 h8;
+                        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[1], (h8)xe[0], acc[u], 0, 0, 0);
+                        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[0], (h8)xe[1], acc[u], 0, 0, 0);
+                        acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[0], (h8)xe[0], acc[u], 0, 0, 0);
+                        continue;
                     }
                     // small terms first: 2^-18 (lo.hi, mid.mid, hi.lo), 2^-9 (mid.hi, hi.mid), 1 (hi.hi)
                     if constexpr (NP == 3) {
@@ -513,10 +585,19 @@ int tiles_for(int N) { return (N + 15) / 16; }
 
 template <typename Real, int NT, int NW, int VAR, int MINW = 1, int SG = 1>
 int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+    constexpr bool hf = (VAR & V_F16X3) != 0;
     constexpr bool bf = (VAR & (V_BF16X6 | V_BF16X3)) != 0;
     constexpr bool frag_regs = (VAR & V_FRAG_REGS) != 0;
     size_t lds;
-    if constexpr (bf) {
+    if constexpr (hf) {
+        const int total = NT * (NT / 2) * 64;
+        float* scl = static_cast<float*>(ws) + hf_scale_offset(NT);
+        hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(256), 0, st, sc, ka.N, scl);
+        hipLaunchKernelGGL((build_frag_f16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
+                           static_cast<const float*>(scl), static_cast<f16x8*>(ws));
+        lds = (frag_regs ? 0 : (size_t)NT * (NT / 2) * 2 * 64 * 16) +
+              (NW > 1 ? (size_t)SG * 2 * (NT / 2) * 2 * 64 * 16 : 0);
+    } else if constexpr (bf) {
         const int total = NT * (NT / 2) * 64;
         hipLaunchKernelGGL((build_frag_bf16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
                            static_cast<bf16x8*>(ws));
@@ -542,7 +623,7 @@ int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
 }
 
 // ---------------- product configurations ----------------
-constexpr int kVarF32 = V_BF16X6 | V_FRAG_REGS | V_KAHAN_A;
+constexpr int kVarF32 = V_F16X3 | V_FRAG_REGS | V_KAHAN_A;
 constexpr int kVarF64 = 0;
 
 size_t frag_bytes(int N, int precision) {
@@ -568,7 +649,7 @@ int cu_count() {
 // share the LDS connectome image (<= 155 / 128 registers): every simulation is
 // resident at once (a single round of workgroups, no tail) at 3-4 waves/SIMD.
 int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
-    constexpr int V = V_BF16X6 | V_KAHAN_A;
+    constexpr int V = V_F16X3 | V_KAHAN_A;
     const int groups = (ka.B + kSims - 1) / kSims;
     const int cus = cu_count();
     if (groups <= 2 * cus) return launch_v<float, 6, 3, kVarF32>(ka, sc, ws, st);
@@ -634,6 +715,12 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 21: return launch_v<float, 6, 3, V_BF16X6 | K | V_REC2, 1, 5>(ka, sc, ws, st);
         case 22: return launch_v<float, 6, 3, V_BF16X6 | V_FRAG_REGS | K | V_REC4>(ka, sc, ws, st);
         case 23: return launch_v<float, 6, 3, V_BF16X6 | K, 1, 5>(ka, sc, ws, st);  // = 15, node-major records
+        // ablations of the grouped product kernel (15): noise off, coupling off
+        case 24: return launch_v<float, 6, 3, V_BF16X6 | K | V_NO_RNG, 1, 5>(ka, sc, ws, st);
+        case 25: return launch_v<float, 6, 3, V_BF16X6 | K | V_NO_MFMA, 1, 5>(ka, sc, ws, st);
+        // fp16 x3 coupling: grouped (as 15), register-resident (as 3)
+        case 26: return launch_v<float, 6, 3, V_F16X3 | K, 1, 5>(ka, sc, ws, st);
+        case 27: return launch_v<float, 6, 3, V_F16X3 | V_FRAG_REGS | K>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
