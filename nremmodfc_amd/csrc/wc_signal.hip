@@ -65,7 +65,41 @@ __device__ __forceinline__ double iir_step(double z[4], double x, const double* 
     z[3] = x * b[4] - y * a[4];
     return y;
 }
+// the same step for b[1] == b[3] == 0 (the Bessel band-pass): z + x*0 - y*a == z - y*a
+// exactly for finite x, so the result is bit-identical with two multiplies fewer
+__device__ __forceinline__ double iir_step_bp(double z[4], double x, const double* b, const double* a) {
+    const double y = z[0] + x * b[0];
+    z[0] = z[1] - y * a[1];
+    z[1] = z[2] + x * b[2] - y * a[2];
+    z[2] = z[3] - y * a[3];
+    z[3] = x * b[4] - y * a[4];
+    return y;
+}
 #pragma clang fp contract(on)
+
+// e^x for the Balloon's (1 - E0)^(1/f) (|x| < 700): x = k ln2 + r, |r| <= ln2/2,
+// e^r by its degree-13 Taylor polynomial (truncation < 2e-17 relative), 2^k by
+// ldexp.  Straight-line, no special cases (ocml's exp spends ~20 more instructions
+// on range checks and coefficient moves).
+__device__ __forceinline__ double exp_rr(double x) {
+    const double k = __builtin_rint(x * 1.4426950408889634);
+    const double r = fma(-k, 1.9082149292705877e-10, fma(-k, 0.6931471803691238, x));  // ln2 hi + lo
+    double p = 1.6059043836821613e-10;                                                 // 1/13!
+    p = fma(p, r, 2.08767569878681e-09);
+    p = fma(p, r, 2.505210838544172e-08);
+    p = fma(p, r, 2.755731922398589e-07);
+    p = fma(p, r, 2.7557319223985893e-06);
+    p = fma(p, r, 2.48015873015873e-05);
+    p = fma(p, r, 1.984126984126984e-04);
+    p = fma(p, r, 1.388888888888889e-03);
+    p = fma(p, r, 8.333333333333333e-03);
+    p = fma(p, r, 4.1666666666666664e-02);
+    p = fma(p, r, 1.6666666666666666e-01);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return __builtin_ldexp(p, (int)k);
+}
 
 struct BoldArgs {
     wc_bold_cfg cfg;
@@ -116,8 +150,8 @@ __device__ __forceinline__ void emit(const BoldArgs& a, const BoldLayout& L, dou
 // COPY: time-major fp32 input, also written out node-major (copy[c*copy_ld + tt])
 // through a 256-column x 32-sample LDS tile flushed as 128-B rows.
 constexpr int kCopyT = 32;
-template <typename ET, bool COPY>
-__global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, int64_t e_ld,
+template <typename ET, bool COPY, bool STEADY, bool BP = false>
+__global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? 3 : 4) : 1) bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, int64_t e_ld,
                                                          int64_t t0, int64_t Tc, double* __restrict__ st,
                                                          float* __restrict__ copy, int64_t copy_ld) {
     const int64_t c0 = (int64_t)blockIdx.x * blockDim.x;
@@ -138,19 +172,33 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
     // lgkmcnt drain orders the tile's writes and reads (a wavefront-scope release
     // fence would also drain the in-flight row stores: 7 ms per chunk at C3)
     auto wsync = []() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    // the wave's rows of the copy through one buffer descriptor (wave-uniform base,
+    // 32-bit per-lane offsets): columns past C fall outside its range and the
+    // hardware drops their stores, so the row loop carries no column test and no
+    // 64-bit addresses (hoisted 64-bit row addresses cost ~100 VGPRs)
+    const int64_t w0u = ((int64_t)__builtin_amdgcn_readfirstlane((uint32_t)(w0 >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)w0);
+    const int64_t ncol = COPY ? (a.C - w0u < 64 ? (a.C > w0u ? a.C - w0u : 0) : 64) : 0;  // 0: no stores
+    const __amdgpu_buffer_rsrc_t crs =
+        __builtin_amdgcn_make_buffer_rsrc(COPY ? copy + w0u * copy_ld : nullptr, 0, (int)(ncol * copy_ld * 4),
+                                          0x00020000);
     auto flush = [&](int64_t tt0, int len) {  // tile samples [tt0, tt0+len) of the wave's columns
         wsync();
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int q = lane + 64 * i, col = q >> 3, part = q & 7;
-            if (w0 + col < a.C && 4 * part < len) {
-                const float* srow = tile + col * (kCopyT + 1) + 4 * part;
-                float* d = copy + (w0 + col) * copy_ld + tt0 + 4 * part;
-                if (vec && 4 * part + 4 <= len) {
-                    *reinterpret_cast<float4*>(d) = make_float4(srow[0], srow[1], srow[2], srow[3]);
-                } else {
-                    for (int k = 0; 4 * part + k < len; ++k) d[k] = srow[k];
-                }
+            const float* srow = tile + col * (kCopyT + 1) + 4 * part;
+            const int off = (int)(((int64_t)col * copy_ld + tt0 + 4 * part) * 4);
+            if (vec && len == kCopyT) {
+                typedef unsigned u4 __attribute__((ext_vector_type(4)));
+                const u4 v = {__float_as_uint(srow[0]), __float_as_uint(srow[1]), __float_as_uint(srow[2]),
+                              __float_as_uint(srow[3])};
+                __builtin_amdgcn_raw_buffer_store_b128(v, crs, off, 0, 0);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * part + k < len) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(srow[k]), crs,
+                                                                                   off + 4 * k, 0, 0);
             }
         }
         wsync();
@@ -176,15 +224,15 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
             m_blk = i0 / a.cfg.dec;
         }
     }
-    // one sample of the stream (x = E at sample tt of this chunk)
-    auto sample = [&](double x, int64_t tt) {
-        const int64_t t = t0 + tt;
-        // Balloon-Windkessel: BOLD[t] from the state after t steps (see oracle/wc_oracle.c orc_bold)
+    // Balloon-Windkessel: BOLD[t] from the state after t steps, then one Euler step
+    // driven by x (see oracle/wc_oracle.c orc_bold)
+    auto balloon = [&](double x) -> double {
         double iv, vpow, vpow_iv;
-        if (a.alpha_3125) {
-            // z = v^(-1/8): fp32 seed, two division-free Newton steps z <- z (1 + (1 - v z^8)/8)
-            // (relative error ~1e-16); then 1/v = z^8 and v^(1/alpha) = v^3.125 = v^4 z^7
-            double z = (double)__builtin_amdgcn_rsqf(__builtin_sqrtf(__builtin_sqrtf((float)v)));
+        if (STEADY || a.alpha_3125) {  // the host launches STEADY only when 1/alpha == 3.125
+            // z = v^(-1/8): fp32 seed (hardware sqrt/rsq), two division-free Newton steps
+            // z <- z (1 + (1 - v z^8)/8) (relative error ~1e-16); then 1/v = z^8 and
+            // v^(1/alpha) = v^3.125 = v^4 z^7
+            double z = (double)__builtin_amdgcn_rsqf(__builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf((float)v)));
 #pragma unroll
             for (int it = 0; it < 2; ++it) {
                 const double z2 = z * z, z4 = z2 * z2;
@@ -203,7 +251,7 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
         double rf = (double)__builtin_amdgcn_rcpf((float)f);  // 1/f: fp32 seed + two Newton steps
         rf = fma(rf, fma(-f, rf, 1.0), rf);
         rf = fma(rf, fma(-f, rf, 1.0), rf);
-        const double fpow = exp(a.log1mEo * rf);
+        const double fpow = exp_rr(a.log1mEo * rf);  // (1 - E0)^(1/f)
         const double ds = x - a.itaus * s - a.itauf * (f - 1.0);
         const double dv = (f - vpow) * a.itauo;
         const double dq = (f * (1.0 - fpow) * a.iEo - q * vpow_iv) * a.itauo;
@@ -212,6 +260,12 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
         f += dt * df;
         v += dt * dv;
         q += dt * dq;
+        return bold;
+    };
+    // one sample of the stream (x = E at sample tt of this chunk), every case
+    auto sample = [&](double x, int64_t tt) {
+        const int64_t t = t0 + tt;
+        const double bold = balloon(x);
         if (t < neq) return;
         const int64_t i = t - neq;  // data index of this BOLD sample
         const int64_t r_cur = r_blk, m_cur = m_blk;
@@ -249,30 +303,88 @@ __global__ void __launch_bounds__(256) bold_chunk_kernel(const BoldArgs a, const
             for (int k = 0; k < 4; ++k) st[L.zend + k * a.C + c] = zb[k];
         }
     };
-    // samples are loaded 16 at a time ahead of their use; with COPY, each batch is
-    // loaded BEFORE the previous 32-sample tile's row stores are issued: vmcnt
-    // retires in issue order, so a load issued after those stores would wait for
-    // them (that ordering cost 7 ms per chunk at C3)
-    for (int64_t tb = 0; tb < Tc; tb += 16) {
-        float xr[16];
-        double xd[16];
+    // steady state (16 <= i <= n - 17: no head/tail bookkeeping, no odd extensions):
+    // Balloon, forward IIR, block summaries; the block-end store is the only branch
+    // (no divergent branch around it: the block counters and the table address stay
+    // wave-uniform, in SGPRs; tail lanes of a COPY launch compute on a shadow column
+    // and only their stores are masked)
+    auto steady = [&](double x, int64_t r, int64_t m) {  // r, m: (block position, block) of the sample
+        const double bold = balloon(x);
+        const double y = BP ? iir_step_bp(zf, bold, b, fa) : iir_step(zf, bold, b, fa);
+        const double* tab = st + L.tab + 5 * r;  // wave-uniform address: scalar loads
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int64_t tt = tb + j < Tc ? tb + j : tb;
-            const ET v = E[e_ld ? ce * e_ld + tt : tt * a.C + ce];
-            if constexpr (sizeof(ET) == 4) xr[j] = v; else xd[j] = v;
+        for (int j = 0; j < 5; ++j) acc[j] += tab[j] * y;
+        if (r == a.cfg.dec - 1) {
+            if (live) {
+                st[L.yzs + m * L.C + c] = acc[0];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) st[L.u + (m * 4 + j) * L.C + c] = acc[1 + j];
+            }
+#pragma unroll
+            for (int j = 0; j < 5; ++j) acc[j] = 0.0;
         }
+    };
+    // Samples come in batches of 16, software-pipelined: batch k+1 is loaded while
+    // batch k is integrated, so the load latency overlaps the fp64 chain.  With COPY
+    // the next batch's loads are also issued BEFORE the previous 32-sample tile's
+    // row stores: vmcnt retires in issue order, so a load issued after those stores
+    // would wait for them (that ordering cost 7 ms per chunk at C3).
+    auto load = [&](ET (&x)[16], int64_t tb) {
+        if (sizeof(ET) == 4 && e_ld == 0) {
+            // time-major fp32: one descriptor per batch (uniform base E + tb*C, the row
+            // offset j*C*4 in an SGPR), the lane's column offset in one VGPR
+            const int64_t nrow = Tc - tb < 16 ? Tc - tb : 16;
+            const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<ET*>(E) + tb * a.C, 0, (int)(nrow * a.C * 4), 0x00020000);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int jj = j < nrow ? j : 0;
+                const uint32_t u = __builtin_amdgcn_raw_buffer_load_b32(ers, (int)(ce * 4), (int)(jj * a.C * 4), 0);
+                x[j] = (ET)__uint_as_float(u);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int64_t tt = tb + j < Tc ? tb + j : tb;
+                x[j] = E[e_ld ? ce * e_ld + tt : tt * a.C + ce];
+            }
+        }
+    };
+    // STEADY launches cover only 16 <= i <= n - 17 (the host splits the chunk)
+    auto process = [&](const ET (&x)[16], int64_t tb) {
         const int k0 = (int)(tb % kCopyT);
         if constexpr (COPY) {
             if (k0 == 0 && tb > 0) flush(tb - kCopyT, kCopyT);
         }
+        // STEADY: (position in block, block) of the batch's first sample, uniform scalars
+        const int64_t ib = t0 + tb - neq, dec = a.cfg.dec;
+        int64_t mb = STEADY ? ib / dec : 0, rb = STEADY ? ib - mb * dec : 0;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            if (tb + j < Tc) {
-                const double x = sizeof(ET) == 4 ? (double)xr[j] : xd[j];
-                if constexpr (COPY) tile[lane * (kCopyT + 1) + k0 + j] = xr[j];
-                if (live) sample(x, tb + j);
+            if constexpr (COPY) tile[lane * (kCopyT + 1) + k0 + j] = (float)x[j];
+            if (STEADY) {
+                if (tb + j < Tc) steady((double)x[j], rb, mb);
+                if (++rb == dec) {
+                    rb = 0;
+                    ++mb;
+                }
+            } else {
+                if (live && tb + j < Tc) sample((double)x[j], tb + j);
             }
+        }
+    };
+    ET xa[16];
+    load(xa, 0);
+    for (int64_t tb = 0; tb < Tc; tb += 16) {
+        if (STEADY) {
+            ET xb[16];
+            if (tb + 16 < Tc) load(xb, tb + 16);
+            process(xa, tb);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) xa[j] = xb[j];
+        } else {
+            if (tb > 0) load(xa, tb);
+            process(xa, tb);
         }
     }
     if constexpr (COPY) {
@@ -804,6 +916,20 @@ int check_cfg(const wc_bold_cfg* cfg, int64_t C) {
     return WC_OK;
 }
 
+template <typename ET, bool COPY>
+void launch_chunk(bool steady, bool bp, dim3 g, hipStream_t st, const BoldArgs& a, const ET* e, int64_t e_ld,
+                  int64_t t0, int64_t len, double* state, float* c, int64_t copy_ld) {
+    if (!steady)
+        hipLaunchKernelGGL((bold_chunk_kernel<ET, COPY, false, false>), g, dim3(256), 0, st, a, e, e_ld, t0, len, state,
+                           c, copy_ld);
+    else if (bp)
+        hipLaunchKernelGGL((bold_chunk_kernel<ET, COPY, true, true>), g, dim3(256), 0, st, a, e, e_ld, t0, len, state,
+                           c, copy_ld);
+    else
+        hipLaunchKernelGGL((bold_chunk_kernel<ET, COPY, true, false>), g, dim3(256), 0, st, a, e, e_ld, t0, len, state,
+                           c, copy_ld);
+}
+
 BoldArgs make_bold_args(const wc_bold_cfg* cfg, int64_t C) {
     BoldArgs a;
     a.cfg = *cfg;
@@ -866,16 +992,37 @@ int wc_bold_chunk(const wc_bold_cfg* cfg, int64_t C, const void* E, int e_f64, i
     const dim3 grid((unsigned)((C + 255) / 256));
     if (copy && (e_f64 || e_ld != 0 || copy_ld < Tc))
         return wc_set_err(WC_EINVAL, "wc_bold_chunk: copy needs fp32 time-major E and copy_ld >= Tc");
+    // 32-bit buffer offsets: 16 rows of fp32 time-major E, 64 rows of the copy
+    if ((!e_f64 && e_ld == 0 && C > (INT32_MAX / 64)) || (copy && copy_ld > INT32_MAX / 256))
+        return wc_set_err(WC_EINVAL, "wc_bold_chunk: C or copy_ld too large for 32-bit buffer offsets");
     float* cp = static_cast<float*>(copy);
-    if (e_f64)
-        hipLaunchKernelGGL((bold_chunk_kernel<double, false>), grid, dim3(256), 0, st, a,
-                           static_cast<const double*>(E), e_ld, t0, Tc, state, cp, copy_ld);
-    else if (copy)
-        hipLaunchKernelGGL((bold_chunk_kernel<float, true>), grid, dim3(256), 0, st, a, static_cast<const float*>(E),
-                           e_ld, t0, Tc, state, cp, copy_ld);
-    else
-        hipLaunchKernelGGL((bold_chunk_kernel<float, false>), grid, dim3(256), 0, st, a, static_cast<const float*>(E),
-                           e_ld, t0, Tc, state, cp, copy_ld);
+    // split [t0, t0+Tc) into the steady range (data index 16 <= i <= n-17: Balloon,
+    // IIR and block sums only) and the rest (pre-equilibration samples, the head
+    // with the front odd extension, the tail with the back one)
+    const int64_t n = cfg->n_total - cfg->neq;
+    const int64_t ts = std::max(t0, cfg->neq + 16), te = std::min(t0 + Tc, cfg->neq + n - 16);
+    const bool steady_ok = a.alpha_3125 != 0;           // the STEADY balloon assumes 1/alpha == 3.125
+    const bool bp = cfg->b[1] == 0.0 && cfg->b[3] == 0.0;  // band-pass zeros at +-1 (b = b0 (1,0,-2,0,1))
+    auto seg = [&](int64_t s0, int64_t len, bool steady) {
+        if (len <= 0) return;
+        if (e_f64) {
+            launch_chunk<double, false>(steady, bp, grid, st, a, static_cast<const double*>(E) + (e_ld ? s0 : s0 * C),
+                                        e_ld, t0 + s0, len, state, nullptr, copy_ld);
+        } else {
+            const float* e = static_cast<const float*>(E) + (e_ld ? s0 : s0 * C);
+            if (cp)
+                launch_chunk<float, true>(steady, bp, grid, st, a, e, e_ld, t0 + s0, len, state, cp + s0, copy_ld);
+            else
+                launch_chunk<float, false>(steady, bp, grid, st, a, e, e_ld, t0 + s0, len, state, nullptr, copy_ld);
+        }
+    };
+    if (steady_ok && ts < te) {
+        seg(0, ts - t0, false);
+        seg(ts - t0, te - ts, true);
+        seg(te - t0, t0 + Tc - te, false);
+    } else {
+        seg(0, Tc, false);
+    }
     return wc_hip_check("wc_bold_chunk");
 }
 

@@ -25,6 +25,8 @@ def main():
     nm = 0.2 + 0.1 * torch.rand(C * ld, dtype=torch.float32, device="cuda")
     tm = 0.2 + 0.1 * torch.rand(1000 * C, dtype=torch.float32, device="cuda")
     bs = BoldStream(C, 300_000, 2000, 1000, 0.04, "cuda")
+    for _ in range(3):  # past Neq and the head: the timed chunks are steady state
+        bs.feed(tm, 1000)
     for name, fn in (("node-major", lambda: bs.feed(nm, 1000, e_ld=ld, offset=0)),
                      ("time-major", lambda: bs.feed(tm, 1000)),
                      ("time-major+copy", lambda: bs.feed(tm, 1000, copy=nm, copy_ld=ld, copy_offset=1000))):
