@@ -147,6 +147,17 @@ int wc_bold_chunk(const wc_bold_cfg* cfg, int64_t C, const void* E, int e_f64, i
                   int64_t t0, int64_t Tc, double* state, void* copy, int64_t copy_ld, void* stream);
 int wc_bold_finish(const wc_bold_cfg* cfg, int64_t C, const double* state, double* out, void* stream);
 
+/* Hierarchical module analysis of B FC matrices, batched (run_many_seeds.py:
+ * 130-133 over HMA.Functional_HP / Balance / nodal_measures, HMA.py:30-203).
+ * fc [B][N][N] fp64 (N <= 96): read, then clipped in place (FC[FC < 0] = 0,
+ * as HMA.py:55 does to the caller's matrix).  Outputs: hin[B], hse[B]
+ * (Balance), hin_node[B][N], hse_node[B][N] (nodal_measures); optional
+ * clus_num [B][N-1] int32 (Functional_HP's Clus_num) and sv [B][N] (singular
+ * values of the symmetrised positive part, descending).  Eigen-decomposition
+ * by cyclic Jacobi in LDS, one workgroup per matrix. */
+int wc_hma(int B, int N, double* fc, double* hin, double* hse, double* hin_node, double* hse_node,
+           int* clus_num, double* sv, void* stream);
+
 /* Unit phasors exp(i angle(hilbert(x, axis=0))) of every column of x [M][C]
  * (utils.kuramoto, utils.py:35-37): phasor [M][C][2] (cos, sin).  workspace:
  * >= M doubles. */

@@ -8,11 +8,11 @@ exec/eval of generated variable names; here the tree is plain lists, with the
 same ordering (level k+1 lists, for every module of level k in order, its
 negative part then its positive part; empty modules dropped).
 
-Runs on the host (numpy SVD of one N x N matrix per simulation): it is the
-per-simulation epilogue of run_many_seeds.py:130-133,
-three 90x90 SVDs per simulation.  Like the reference, every function clips the
-caller's FC in place (FC[FC < 0] = 0, HMA.py:55) -- run_many_seeds saves that
-clipped sFC.
+The per-matrix functions run on the host (numpy SVD), with the reference's call
+surface.  The sweep path uses integration_segregation_batch: the same quantities
+for a whole batch in one device launch (wc_hma, nremmodfc_amd/csrc/wc_hma.hip;
+SURVEY.md 8f rank 3).  Like the reference, every function clips the caller's FC
+in place (FC[FC < 0] = 0, HMA.py:55) -- run_many_seeds saves that clipped sFC.
 """
 import numpy as np
 
@@ -87,3 +87,21 @@ def integration_segregation(sFC):
     hin, hse = Balance(sFC, cn, cs)
     hin_n, hse_n = nodal_measures(sFC, cn, cs)
     return {"Hin_sim": hin, "Hse_sim": hse, "Hin_node_sim": hin_n, "Hse_node_sim": hse_n, "sFC": sFC}
+
+
+def integration_segregation_batch(sfcs, device="cuda"):
+    """integration_segregation for a batch [B][N][N] (N <= 96) in one device launch.
+
+    Returns one dict per matrix with the keys run_many_seeds.py:134-136 pickles;
+    sFC is the clipped matrix (as the reference saves it).
+    """
+    import torch
+
+    from . import sigchain
+    fc = torch.as_tensor(np.ascontiguousarray(np.asarray(sfcs, dtype=np.float64))).to(device)
+    r = sigchain.hma(fc)
+    clipped = fc.cpu().numpy()
+    hin, hse = r["hin"].cpu().numpy(), r["hse"].cpu().numpy()
+    hin_n, hse_n = r["hin_node"].cpu().numpy(), r["hse_node"].cpu().numpy()
+    return [{"Hin_sim": np.float64(hin[b]), "Hse_sim": np.float64(hse[b]), "Hin_node_sim": hin_n[b],
+             "Hse_node_sim": hse_n[b], "sFC": clipped[b]} for b in range(fc.shape[0])]

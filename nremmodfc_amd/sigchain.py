@@ -126,6 +126,32 @@ def kuramoto(x, B=1, N=None):
     return out
 
 
+def hma(fc, want_clus_num=False):
+    """HMA integration / segregation of B FC matrices on the device (HMA.py:30-203
+    as run_many_seeds.py:130-133 uses it).
+
+    fc [B][N][N] (or [N][N]) fp64 device tensor, clipped in place (FC < 0 -> 0,
+    as HMA.py:55).  Returns a dict of device tensors: hin [B], hse [B],
+    hin_node [B][N], hse_node [B][N], sv [B][N] (+ clus_num [B][N-1] int32).
+    """
+    L = _lib.lib()
+    if fc.dim() == 2:
+        fc = fc.unsqueeze(0)
+    if fc.dtype != torch.float64 or not fc.is_contiguous():
+        raise _lib.WCSDEError("hma: fc must be a contiguous fp64 device tensor (it is clipped in place)")
+    B, N = fc.shape[0], fc.shape[1]
+    dev = fc.device
+    out = {k: torch.empty(s, dtype=torch.float64, device=dev)
+           for k, s in (("hin", (B,)), ("hse", (B,)), ("hin_node", (B, N)), ("hse_node", (B, N)), ("sv", (B, N)))}
+    cn = torch.empty((B, N - 1), dtype=torch.int32, device=dev) if want_clus_num else None
+    rc = L.wc_hma(B, N, _lib.ptr(fc), _lib.ptr(out["hin"]), _lib.ptr(out["hse"]), _lib.ptr(out["hin_node"]),
+                  _lib.ptr(out["hse_node"]), _lib.ptr(cn), _lib.ptr(out["sv"]), _lib.stream_handle())
+    _lib.check(rc, "wc_hma")
+    if cn is not None:
+        out["clus_num"] = cn
+    return out
+
+
 class WelchAccumulator:
     """Running node-summed |FFT|^2 of 4000-sample Hann segments (welch, nperseg=4000)."""
 

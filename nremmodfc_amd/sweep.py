@@ -265,7 +265,8 @@ def main(argv=None):
     if args.kind == "many":
         from . import HMA
         rows, fcs = run_sims(mine, sc, empfcs, sched, args.precision, args.batch, device, want_fc=True)
-        save = {(s.seed, s.state): HMA.integration_segregation(fc.copy()) for s, fc in zip(mine, fcs)}
+        hma = HMA.integration_segregation_batch(fcs, device) if fcs else []
+        save = {(s.seed, s.state): d for s, d in zip(mine, hma)}
         with open(os.path.join(args.out, "temp", f"{tag}_rank{rank}.pickle"), "wb") as f:
             pickle.dump(save, f)
         if dist:

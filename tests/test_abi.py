@@ -63,3 +63,12 @@ def test_invalid_arguments_fail_loudly():
     assert L.wc_fc_metrics(1, 200, 298, None, None, None, 0, 1.0, None, None, None, None, None) == -1
     assert L.wc_kuramoto(0, 90, 298, None, None, None) == -1
     assert L.wc_welch_bins() == 2001
+
+
+def test_hma_validates_without_device_work():
+    from nremmodfc_amd import _lib
+    L = _lib.lib()
+    vp = ctypes.c_void_p(16)
+    assert L.wc_hma(4, 90, None, vp, vp, vp, vp, None, None, None) == -1
+    assert L.wc_hma(4, 97, vp, vp, vp, vp, vp, None, None, None) == -2
+    assert b"96" in L.wc_last_error()

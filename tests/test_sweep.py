@@ -162,3 +162,10 @@ def test_many_seeds_main_short(tmp_path, cuda):
     assert set(v) == {"Hin_sim", "Hse_sim", "Hin_node_sim", "Hse_node_sim", "sFC"}
     assert v["sFC"].shape == (90, 90) and (v["sFC"] >= 0).all()  # clipped in place like the reference
     assert v["Hin_node_sim"].shape == (90,) and np.isfinite(v["Hin_sim"])
+    # the device-batched HMA (wc_hma) agrees with the host facade on the saved (clipped) sFC
+    from nremmodfc_amd import HMA
+    for k in keys:
+        h = HMA.integration_segregation(d[k]["sFC"].copy())
+        np.testing.assert_allclose(d[k]["Hin_sim"], h["Hin_sim"], rtol=1e-12)
+        np.testing.assert_allclose(d[k]["Hse_sim"], h["Hse_sim"], rtol=1e-11)
+        np.testing.assert_allclose(d[k]["Hse_node_sim"], h["Hse_node_sim"], rtol=1e-9, atol=1e-15)
