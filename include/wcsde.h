@@ -158,6 +158,43 @@ int wc_bold_finish(const wc_bold_cfg* cfg, int64_t C, const double* state, doubl
 int wc_hma(int B, int N, double* fc, double* hin, double* hse, double* hin_node, double* hse_node,
            int* clus_num, double* sv, void* stream);
 
+/* ------------------------------------------------------------------------
+ * SC optimiser (optimize_SC_Hopf.py:47-104), SURVEY.md 8f rank 4.
+ * The Hopf (Stuart-Landau) network of Hopf_model_multi.py:46-156, batched over
+ * simulations (random seeds):
+ *   x' = (a - x^2 - y^2) x - w y + sum_j (G M_ij / norm) (x_j - x_i)
+ *   y' = (a - x^2 - y^2) y + w x + sum_j (G M_ij / norm) (y_j - y_i)
+ *   state += f dt + beta z sqrt(dt)    (Euler-Maruyama, :143-144)
+ * fp64.  Noise: the Philox stream above with the simulation key; node i's
+ * (x, y) normals are the Box-Muller pair (2i, 2i+1), i.e. quad i/2.
+ * x, y [B][N] in/out; when rec_every > 0, x BEFORE every local step s with
+ * s % rec_every == 0 is stored at rec[s / rec_every][B][N] (and y at rec_y,
+ * which may be NULL): a run recorded from its first step gives the
+ * reference's results[k] = state after k*downsamp steps (:140-149).  M is N x N
+ * (row i = inputs of node i); workspace >= wc_hopf_workspace_size(N). */
+typedef struct wc_hopf_params {
+    double a;     /* bifurcation parameter (Hopf_model_multi.py:22) */
+    double w;     /* angular frequency, 0.05 * 2 pi (:23) */
+    double beta;  /* noise scale (:25) */
+    double dt;    /* Euler step (:28) */
+    double G;     /* global coupling (:38; optimize_SC_Hopf.py:39) */
+    double norm;  /* mean column sum of M (:37, optimize_SC_Hopf.py:30,101) */
+} wc_hopf_params;
+
+size_t wc_hopf_workspace_size(int N);
+int wc_hopf_integrate(const wc_hopf_params* p, int B, int N, const double* M, const uint64_t* keys,
+                      double* x, double* y, int64_t step0, int64_t nsteps, int64_t rec_every,
+                      double* rec, double* rec_y, void* workspace, size_t ws_bytes, void* stream);
+
+/* scipy.signal.filtfilt(b, a, x, axis=0) of every column of x [T][C] fp64 ->
+ * y [T][C] (y must not alias x): odd extension of padlen = 3 (order + 1),
+ * lfilter_zi initial conditions zi[order] (host, from the caller), DF2T in
+ * scipy's association order.  order in {2, 4, 6, 8}; b, a, zi are HOST
+ * arrays of order + 1, order + 1 and order doubles, a[0] == 1.
+ * (optimize_SC_Hopf.py:63-66; also any simBOLD-style band-pass.) */
+int wc_filtfilt(int order, const double* b, const double* a, const double* zi, int64_t T, int64_t C,
+                const double* x, double* y, void* stream);
+
 /* Unit phasors exp(i angle(hilbert(x, axis=0))) of every column of x [M][C]
  * (utils.kuramoto, utils.py:35-37): phasor [M][C][2] (cos, sin).  workspace:
  * >= M doubles. */

@@ -1,0 +1,156 @@
+"""Drop-in for the reference's Hopf_model_multi.py (the SC optimiser's network model).
+
+Same module surface (Hopf_model_multi.py:21-187): the globals a, w, beta, dt,
+teq, tmax, downsamp, nnodes, ones_vector, M, norm, G, seed; Sim(verbose) ->
+(results [Nmax][nnodes][2], time_vector); ParamsNode / ParamsNet / ParamsSim.
+Callers mutate the globals and call Sim(), as optimize_SC_Hopf.py:18-39 does.
+
+The Euler-Maruyama loop (Hopf_model :46-59, Noise :63-69, Sim :79-156) runs in
+libwcsde.so (wc_hopf_integrate, csrc/wc_hopf.hip), fp64, batched:
+sim_batch(seeds) integrates one simulation per seed in one launch, which is what
+the optimiser (nremmodfc_amd.optimize_sc) uses.  Hopf_model and Noise are fused
+into that kernel and raise if called on their own.
+
+Deliberate deviations:
+  * noise: the build's Philox stream keyed by the seed (numba's per-thread RNG
+    cannot be reproduced outside numba);
+  * initial conditions: np.random.RandomState(seed).uniform(0.01, 1, (N, 2)), what
+    :121 draws when set_seed() has seeded NumPy's generator (in the jitted
+    reference set_seed only seeds numba's generator, so :121 is unseeded);
+  * the default M (:34) is a Watts-Strogatz graph built with numpy, seeded with 0
+    (the reference calls networkx unseeded; every caller replaces M anyway).
+"""
+import numpy as np
+import torch
+
+from . import _lib
+
+# Model parameters (Hopf_model_multi.py:21-25)
+a = 0.0
+w = 0.05 * 2 * np.pi
+beta = 0.032
+
+# Simulation parameters (:27-31)
+dt = 1e-1
+teq = 60
+tmax = 1200
+downsamp = 1
+
+
+def watts_strogatz(n, k, p, seed=0):
+    """Ring lattice of n nodes joined to their k nearest neighbours, every edge
+    rewired with probability p (networkx.watts_strogatz_graph's algorithm), as a
+    dense 0/1 matrix."""
+    rng = np.random.default_rng(seed)
+    adj = np.zeros((n, n))
+    for j in range(1, k // 2 + 1):
+        for u in range(n):
+            v = (u + j) % n
+            adj[u, v] = adj[v, u] = 1
+    for j in range(1, k // 2 + 1):
+        for u in range(n):
+            v = (u + j) % n
+            if rng.random() < p and adj[u, v]:
+                cand = [x for x in range(n) if x != u and not adj[u, x]]
+                if cand:
+                    nv = cand[rng.integers(len(cand))]
+                    adj[u, v] = adj[v, u] = 0
+                    adj[u, nv] = adj[nv, u] = 1
+    return adj
+
+
+# Network parameters (:33-39)
+nnodes = 90
+ones_vector = np.ones(nnodes).reshape((1, nnodes))
+M = watts_strogatz(nnodes, 8, 0.075)
+norm = np.mean(np.sum(M, 0))
+G = 0.25
+seed = 0
+
+
+def Hopf_model(x, y, t):
+    raise NotImplementedError("Hopf_model is fused into wc_hopf_integrate (libwcsde.so); call Sim()")
+
+
+def Noise(x, y, t):
+    raise NotImplementedError("Noise is drawn inside wc_hopf_integrate (Philox stream); call Sim()")
+
+
+def set_seed(s):
+    """Hopf_model_multi.py:73-76: the seed of the next Sim()."""
+    global seed
+    seed = s
+    return s
+
+
+def initial_conditions(s, n):
+    """(x, y) initial state of seed s: uniform(0.01, 1) per node and variable (:121)."""
+    ic = np.random.RandomState(s).uniform(0.01, 1, (n, 2))
+    return ic[:, 0].copy(), ic[:, 1].copy()
+
+
+def _params():
+    return _lib.WCHopfParamsC(float(a), float(w), float(beta), float(dt), float(G), float(norm))
+
+
+def _check_m():
+    m = np.asarray(M)
+    if m.ndim != 2 or m.shape[0] != m.shape[1] or m.shape[0] != nnodes:
+        raise ValueError("check M dimensions (", m.shape, ") and number of nodes (", nnodes, ")")
+    return np.ascontiguousarray(m, dtype=np.float64)
+
+
+def sim_batch(seeds, want_y=False, device="cuda"):
+    """One Sim() per seed in a single launch.
+
+    Returns x (and y) of the kept samples, time-major [Nmax][B][nnodes] fp64 device
+    tensors: row k is the state after (Neq + k) * downsamp Euler steps, i.e.
+    Sim()'s results[k, :, 0 / 1] (Hopf_model_multi.py:116-149).
+    """
+    L = _lib.lib()
+    m = torch.from_numpy(_check_m()).to(device)
+    n = m.shape[0]
+    seeds = [int(s) for s in seeds]
+    B = len(seeds)
+    neq = int(teq / dt / downsamp)
+    nmax = int(tmax / dt / downsamp)
+    ics = [initial_conditions(s, n) for s in seeds]
+    x = torch.from_numpy(np.stack([c[0] for c in ics])).to(device)
+    y = torch.from_numpy(np.stack([c[1] for c in ics])).to(device)
+    keys = torch.tensor(seeds, dtype=torch.int64, device=device)
+    ws = torch.empty(L.wc_hopf_workspace_size(n) // 8 + 1, dtype=torch.float64, device=device)
+    rx = torch.empty((nmax, B, n), dtype=torch.float64, device=device)
+    ry = torch.empty_like(rx) if want_y else None
+    hp = _params()
+    st = _lib.stream_handle()
+    ds = int(downsamp)
+    # transient: Neq records' worth of steps, nothing kept (results[Neq:], :152)
+    rc = L.wc_hopf_integrate(hp, B, n, _lib.ptr(m), _lib.ptr(keys), _lib.ptr(x), _lib.ptr(y), 0, neq * ds, 0,
+                             None, None, _lib.ptr(ws), ws.numel() * 8, st)
+    _lib.check(rc, "wc_hopf_integrate (transient)")
+    rc = L.wc_hopf_integrate(hp, B, n, _lib.ptr(m), _lib.ptr(keys), _lib.ptr(x), _lib.ptr(y), neq * ds, nmax * ds,
+                             ds, _lib.ptr(rx), _lib.ptr(ry), _lib.ptr(ws), ws.numel() * 8, st)
+    _lib.check(rc, "wc_hopf_integrate")
+    return (rx, ry) if want_y else rx
+
+
+def Sim(verbose=True):
+    """Hopf_model_multi.py:79-156 -> (results [Nmax][nnodes][2], time_vector)."""
+    rx, ry = sim_batch([seed], want_y=True)
+    if verbose:
+        print(f"Elapsed time: {int(tmax + teq)} seconds")
+    results = torch.stack((rx[:, 0, :], ry[:, 0, :]), dim=-1).cpu().numpy()
+    nmax = int(tmax / dt / downsamp)
+    return results, np.linspace(0, tmax, nmax)
+
+
+def ParamsNode():
+    return {"a": a, "beta": beta, "w": w}
+
+
+def ParamsNet():
+    return {"nnodes": nnodes, "G": G, "norm": norm}
+
+
+def ParamsSim():
+    return {"tmax": tmax, "teq": teq, "dt": dt, "downsamp": downsamp, "seed": seed}

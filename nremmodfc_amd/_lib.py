@@ -30,6 +30,11 @@ class WCBoldCfgC(ctypes.Structure):
                 ("zi", ctypes.c_double * 4)]
 
 
+class WCHopfParamsC(ctypes.Structure):
+    """Mirror of ``wc_hopf_params`` (include/wcsde.h)."""
+    _fields_ = [(n, ctypes.c_double) for n in ("a", "w", "beta", "dt", "G", "norm")]
+
+
 class WCSDEError(RuntimeError):
     pass
 
@@ -58,6 +63,11 @@ _SIGNATURES = {
     "wc_fc_metrics": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wc_kuramoto": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "wc_hma": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wc_hopf_workspace_size": (c_sz, [c_int]),
+    "wc_hopf_integrate": (c_int, [ctypes.POINTER(WCHopfParamsC), c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+                                  c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "wc_filtfilt": (c_int, [c_int, ctypes.POINTER(c_dbl), ctypes.POINTER(c_dbl), ctypes.POINTER(c_dbl),
+                            c_i64, c_i64, c_vp, c_vp, c_vp]),
     "wc_welch_workspace_size": (c_sz, []),
     "wc_welch_bins": (c_int, []),
     "wc_welch_prepare": (c_int, [c_vp, c_sz, c_vp]),

@@ -2,7 +2,9 @@
 
 SC_opti_25julio.txt (structural connectome, loaded at whole_sweep_both.py:34),
 empirical/mean_mat_{W,N1,N2,N3}_8dic24.txt (empirical FC, whole_sweep_both.py:36-37)
-and empirical/maps/*.npy (NA/ACh proxy maps, whole_sweep_both_maps.py:44-65).
+empirical/maps/*.npy (NA/ACh proxy maps, whole_sweep_both_maps.py:44-65) and
+empirical/structural_Deco_AAL.txt (the SC optimiser's starting connectome,
+optimize_SC_Hopf.py:28).
 The SHUFFLED_*_LABELS_*.npy files of the reference are pickled object arrays and
 are not shipped (nothing on the hot path reads them).
 """
@@ -20,6 +22,11 @@ MAPNAMES_NA = ["HOMO", "DIST_LC_proj", "SHUFFLED_SYMM_DIST_LC_proj"]
 
 def load_sc():
     return np.load(os.path.join(DATA, "SC_opti_25julio.npy"))
+
+
+def load_deco_sc():
+    """empirical/structural_Deco_AAL.txt (optimize_SC_Hopf.py:28)."""
+    return np.load(os.path.join(DATA, "structural_Deco_AAL.npy"))
 
 
 def load_empfc(state):

@@ -27,6 +27,10 @@ class OrcParams(ctypes.Structure):
         "sqdtD", "dtSim")]
 
 
+class OrcHopfParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in ("a", "w", "beta", "dt", "G", "norm")]
+
+
 def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB
@@ -54,6 +58,10 @@ def lib():
                                              ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
                                              ctypes.c_int64, dp, ctypes.c_int]
         l.orc_bold.argtypes = [dp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, dp]
+        l.orc_hopf_integrate_batch.restype = ctypes.c_int
+        l.orc_hopf_integrate_batch.argtypes = [ctypes.POINTER(OrcHopfParams), ctypes.c_int, ctypes.c_int, dp,
+                                               ctypes.POINTER(ctypes.c_uint64), dp, dp, ctypes.c_int64,
+                                               ctypes.c_int64, ctypes.c_int64, dp]
         _lib = l
     return _lib
 
@@ -129,3 +137,19 @@ def bold(E_t, dt):
     out = np.empty_like(E_t)
     lib().orc_bold(_dp(E_t), T, N, float(dt), _dp(out))
     return out
+
+
+def hopf_integrate(params, M, keys, x, y, step0, nsteps, rec_every=0):
+    """Batched Hopf network (orc_hopf_integrate_batch).  params: dict a, w, beta, dt, G,
+    norm; M [N][N]; x, y [B][N] updated in place.  Returns rec [B][n_rec][N] or None."""
+    B, N = x.shape
+    M = np.ascontiguousarray(M, dtype=np.float64)
+    k = np.ascontiguousarray(keys, dtype=np.uint64)
+    n_rec = -(-nsteps // rec_every) if rec_every else 0
+    rec = np.empty((B, n_rec, N)) if rec_every else None
+    hp = OrcHopfParams(*(float(params[n]) for n in ("a", "w", "beta", "dt", "G", "norm")))
+    rc = lib().orc_hopf_integrate_batch(ctypes.byref(hp), B, N, _dp(M),
+                                        k.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), _dp(x), _dp(y),
+                                        int(step0), int(nsteps), int(rec_every), _dp(rec))
+    assert rc == 0
+    return rec

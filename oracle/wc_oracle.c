@@ -181,6 +181,62 @@ int orc_wc_integrate_batch(const orc_params* p, int B, int N, const double* sc, 
     return err ? -1 : 0;
 }
 
+/* ---------------- Hopf network (SC optimiser) ----------------
+ * Restates Hopf_model_multi.py:46-59 (Hopf_model), :63-69 (Noise) and the
+ * Euler-Maruyama update of Sim (:143-144, results_temp += f dt + noise sqrt(dt)):
+ *   Isyn_i = sum_j (G * M_ij / norm) * (x_j - x_i)            (:49-53)
+ *   x' = (a - x^2 - y^2) x - w y + IsynX,  y' = (a - x^2 - y^2) y + w x + IsynY
+ * with the numba RNG replaced by the Philox stream (node i's (x, y) normals =
+ * Box-Muller pair (2i, 2i+1) = quad i/2).  x BEFORE local step s is stored at
+ * rec[s / rec_every] when s % rec_every == 0.  Parity status: the reference
+ * module needs numba and networkx (absent), so it is pinned by the analytic
+ * noise-free solution (tests/test_oracle_hopf.py), not by running it. */
+typedef struct orc_hopf_params { double a, w, beta, dt, G, norm; } orc_hopf_params;
+
+int orc_hopf_integrate(const orc_hopf_params* p, int N, const double* M, uint64_t key, double* x, double* y,
+                       int64_t step0, int64_t nsteps, int64_t rec_every, double* rec)
+{
+    if (N <= 0 || N > 4096) return -1;
+    static const int kMax = 4096;
+    double nx[kMax], ny[kMax], z[kMax + 4];
+    const double sqdt = sqrt(p->dt);
+    for (int64_t s = 0; s < nsteps; ++s) {
+        if (rec_every > 0 && s % rec_every == 0) memcpy(rec + (s / rec_every) * N, x, sizeof(double) * N);
+        for (int q = 0; 2 * q < N; ++q) quad_normals(key, step0 + s, (uint32_t)q, z + 4 * q);
+        for (int i = 0; i < N; ++i) {
+            double cx = 0.0, cy = 0.0;
+            for (int j = 0; j < N; ++j) {
+                const double m = p->G * M[(size_t)i * N + j] / p->norm;
+                cx += m * (x[j] - x[i]);
+                cy += m * (y[j] - y[i]);
+            }
+            const double r = p->a - x[i] * x[i] - y[i] * y[i];
+            const double fx = r * x[i] - p->w * y[i] + cx;
+            const double fy = r * y[i] + p->w * x[i] + cy;
+            nx[i] = x[i] + (fx * p->dt + (z[2 * i] * p->beta) * sqdt);
+            ny[i] = y[i] + (fy * p->dt + (z[2 * i + 1] * p->beta) * sqdt);
+        }
+        memcpy(x, nx, sizeof(double) * N);
+        memcpy(y, ny, sizeof(double) * N);
+    }
+    return 0;
+}
+
+/* B simulations (x, y [B][N], rec [B][n_rec][N] or NULL), parallel over sims */
+int orc_hopf_integrate_batch(const orc_hopf_params* p, int B, int N, const double* M, const uint64_t* keys,
+                             double* x, double* y, int64_t step0, int64_t nsteps, int64_t rec_every, double* rec)
+{
+    const int64_t n_rec = rec_every > 0 ? (nsteps + rec_every - 1) / rec_every : 0;
+    int err = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+    for (int b = 0; b < B; ++b)
+        err |= orc_hopf_integrate(p, N, M, keys[b], x + (size_t)b * N, y + (size_t)b * N, step0, nsteps,
+                                  rec_every, rec ? rec + (size_t)b * n_rec * N : NULL);
+    return err ? -1 : 0;
+}
+
 /* Balloon-Windkessel BOLD (assumed form of the missing BOLDModel.BD.Sim, see
  * DESIGN.md "BOLD model"): Euler at dt per E sample, y0 = (s,f,v,q) = (0,1,1,1),
  * BOLD[t] computed from the state after t steps.  rE is [T][N]; out is [T][N]. */

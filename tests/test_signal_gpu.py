@@ -228,3 +228,15 @@ def test_pipeline_fc_ssim_vs_oracle(cuda, sc90):
     for b in range(len(keys)):
         _, _, wfc = osg.sim_metrics(rec[b], emp)
         assert osg.ssim(res.fc[b], wfc, data_range=2.0) >= 0.999999
+
+
+@pytest.mark.parametrize("M", [6000, 777])
+def test_fc_long_series_vs_numpy(cuda, M):
+    """wc_fc_metrics' corrcoef over long series (the SC optimiser's 6000-sample window)."""
+    rng = np.random.default_rng(M)
+    B, N = 3, 90
+    x = rng.standard_normal((M, B, N)).cumsum(0) * 0.01 + rng.standard_normal((1, B, N))
+    fc, _, _ = wsg.fc_metrics(torch.from_numpy(x).cuda(), B, N, None, kuramoto=False, want_fc=True)
+    fc = fc.cpu().numpy()
+    for b in range(B):
+        np.testing.assert_allclose(fc[b], np.corrcoef(x[:, b, :].T), rtol=0, atol=1e-12)
