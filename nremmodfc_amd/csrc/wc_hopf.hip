@@ -12,7 +12,7 @@
 //     (order-2K IIR, odd extension of padlen = 3 max(len(a), len(b)),
 //      lfilter_zi initial conditions: the published SciPy algorithm).
 //
-// Hopf layout: one workgroup per simulation, one thread per node; x, y in
+// Hopf layout: one workgroup per simulation, four lanes per node (N <= 256); x, y in
 // registers for the whole launch, G M / norm transposed in LDS (conflict-free
 // column reads), the node states exchanged through a double-buffered LDS image
 // (one barrier per step).  Noise: the build's Philox4x32-10 stream
@@ -56,59 +56,68 @@ __global__ void hopf_weights_kernel(const double* __restrict__ M, int N, double 
     mg[idx] = G * M[(size_t)i * N + j] / norm;
 }
 
-template <bool LDS>
+// LPN lanes per node (adjacent lanes): lane q of node i sums j = q, q + LPN, ...; two
+// xor-shuffles combine the partial sums (commutative: every lane gets the same bits),
+// and every lane then carries the same x, y; lane 0 publishes and records.
+template <bool LDS, int LPN>
 __global__ void __launch_bounds__(kHopfMaxN) hopf_kernel(const HopfArgs p) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int N = p.N;
-    const int i = threadIdx.x;
+    const int i = threadIdx.x / LPN, q = threadIdx.x % LPN;
     const int b = blockIdx.x;
     const bool live = i < N;
+    const bool lead = live && q == 0;
     double* xs = sm + (LDS ? (size_t)N * N : 0);  // [2][N]
     double* ys = xs + 2 * N;                     // [2][N]
     const double* mg = p.mg;
     if constexpr (LDS) {
         double* l = sm;
-        for (int k = i; k < N * N; k += blockDim.x) l[k] = p.mg[k];
+        for (int k = threadIdx.x; k < N * N; k += blockDim.x) l[k] = p.mg[k];
         mg = l;
     }
-    double x = live ? p.x[(size_t)b * N + i] : 0.0;
-    double y = live ? p.y[(size_t)b * N + i] : 0.0;
+    const int ii = live ? i : N - 1;  // tail lanes shadow the last node, never store
+    double x = p.x[(size_t)b * N + ii];
+    double y = p.y[(size_t)b * N + ii];
     const uint64_t key = p.keys[b];
     const double a = p.a, w = p.w, dt = p.dt, bs = p.beta;
     for (int64_t s = 0; s < p.nsteps; ++s) {
         const int buf = (int)(s & 1);
-        if (p.rec_every > 0 && s % p.rec_every == 0 && live) {
+        if (p.rec_every > 0 && s % p.rec_every == 0 && lead) {
             const int64_t o = ((s / p.rec_every) * p.B + b) * (int64_t)N + i;
             p.rec[o] = x;
             if (p.rec_y) p.rec_y[o] = y;
         }
-        if (live) {
+        if (lead) {
             xs[buf * N + i] = x;
             ys[buf * N + i] = y;
         }
+        // the step's normals do not depend on the state: drawn before the barrier wait
+        double z[4];
+        wcdev::quad_normals((uint64_t)(p.step0 + s), (uint32_t)(ii >> 1), key, z);
         __syncthreads();  // also orders the LDS weight image before the first step
-        if (live) {
-            // Isyn_i = sum_j (G M_ij / norm) (x_j - x_i)    (Hopf_model_multi.py:49-53)
-            double cx = 0.0, cy = 0.0;
-            const double* xb = xs + buf * N;
-            const double* yb = ys + buf * N;
-            for (int j = 0; j < N; ++j) {
-                const double m = mg[(size_t)j * N + i];
-                cx += m * (xb[j] - x);
-                cy += m * (yb[j] - y);
-            }
-            double z[4];
-            wcdev::quad_normals((uint64_t)(p.step0 + s), (uint32_t)(i >> 1), key, z);
-            const double zx = z[2 * (i & 1)], zy = z[2 * (i & 1) + 1];
-            const double r = a - x * x - y * y;
-            const double fx = r * x - w * y + cx;   // Hopf_model_multi.py:55
-            const double fy = r * y + w * x + cy;   // :56
-            // results_temp += Hopf_model(...) * dt + Noise(...) * sqrt(dt)   (:143-144)
-            x += fx * dt + (zx * bs) * p.sqdt;
-            y += fy * dt + (zy * bs) * p.sqdt;
+        // Isyn_i = sum_j (G M_ij / norm) (x_j - x_i)    (Hopf_model_multi.py:49-53)
+        double cx = 0.0, cy = 0.0;
+        const double* xb = xs + buf * N;
+        const double* yb = ys + buf * N;
+        for (int j = q; j < N; j += LPN) {
+            const double m = mg[(size_t)j * N + ii];
+            cx += m * (xb[j] - x);
+            cy += m * (yb[j] - y);
         }
+#pragma unroll
+        for (int o = 1; o < LPN; o <<= 1) {
+            cx += __shfl_xor(cx, o);
+            cy += __shfl_xor(cy, o);
+        }
+        const double zx = z[2 * (ii & 1)], zy = z[2 * (ii & 1) + 1];
+        const double r = a - x * x - y * y;
+        const double fx = r * x - w * y + cx;   // Hopf_model_multi.py:55
+        const double fy = r * y + w * x + cy;   // :56
+        // results_temp += Hopf_model(...) * dt + Noise(...) * sqrt(dt)   (:143-144)
+        x += fx * dt + (zx * bs) * p.sqdt;
+        y += fy * dt + (zy * bs) * p.sqdt;
     }
-    if (live) {
+    if (lead) {
         p.x[(size_t)b * N + i] = x;
         p.y[(size_t)b * N + i] = y;
     }
@@ -139,8 +148,8 @@ __global__ void __launch_bounds__(256) filtfilt_kernel(const FiltArgs f) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= f.C) return;
     const int64_t C = f.C, T = f.T;
-    const double* x = f.x + c;
-    double* y = f.y + c;
+    const double* __restrict__ x = f.x + c;
+    double* __restrict__ y = f.y + c;
     double z[K];
     // odd extension in front: ext[k] = 2 x0 - x[PL - k], k = 0..PL-1; zi * ext[0]
     const double x0 = x[0];
@@ -148,7 +157,17 @@ __global__ void __launch_bounds__(256) filtfilt_kernel(const FiltArgs f) {
 #pragma unroll
     for (int k = 0; k < K; ++k) z[k] = f.zi[k] * e0;
     for (int k = 0; k < PL; ++k) df2t<K>(z, 2.0 * x0 - x[(PL - k) * C], f);
-    for (int64_t t = 0; t < T; ++t) y[t * C] = df2t<K>(z, x[t * C], f);
+    // main samples in batches of 16: the batch's loads are issued together (one
+    // latency per batch instead of one per sample: the recursion itself is short)
+    int64_t t = 0;
+    for (; t + 16 <= T; t += 16) {
+        double v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = x[(t + k) * C];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) y[(t + k) * C] = df2t<K>(z, v[k], f);
+    }
+    for (; t < T; ++t) y[t * C] = df2t<K>(z, x[t * C], f);
     // odd extension at the end: 2 x[T-1] - x[T-2-k], k = 0..PL-1 (outputs kept for the backward pass)
     const double xl = x[(T - 1) * C];
     double yt[PL];
@@ -159,7 +178,15 @@ __global__ void __launch_bounds__(256) filtfilt_kernel(const FiltArgs f) {
     for (int k = 0; k < K; ++k) z[k] = f.zi[k] * yt[PL - 1];
 #pragma unroll
     for (int k = PL - 1; k >= 0; --k) df2t<K>(z, yt[k], f);
-    for (int64_t t = T - 1; t >= 0; --t) y[t * C] = df2t<K>(z, y[t * C], f);
+    t = T - 1;
+    for (; t >= 15; t -= 16) {
+        double v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = y[(t - k) * C];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) y[(t - k) * C] = df2t<K>(z, v[k], f);
+    }
+    for (; t >= 0; --t) y[t * C] = df2t<K>(z, y[t * C], f);
 }
 #pragma clang fp contract(on)
 
@@ -188,17 +215,18 @@ int wc_hopf_integrate(const wc_hopf_params* hp, int B, int N, const double* M, c
     p.a = hp->a; p.w = hp->w; p.beta = hp->beta; p.dt = hp->dt; p.sqdt = sqrt(hp->dt);
     p.mg = mg; p.keys = keys; p.x = x; p.y = y; p.rec = rec; p.rec_y = rec_y;
     p.step0 = step0; p.nsteps = nsteps; p.rec_every = rec_every; p.B = B; p.N = N;
-    const int threads = ((N + 63) / 64) * 64;
+    // 4 lanes per node while 4N threads fit one workgroup (N <= 256), else 1
+    const int lpn = N <= kHopfMaxN / 4 ? 4 : 1;
+    const int threads = ((lpn * N + 63) / 64) * 64;
     const bool lds = N <= kHopfLdsN;
     const size_t bytes = ((lds ? (size_t)N * N : 0) + 4 * (size_t)N) * sizeof(double);
-    if (lds) {
-        hipError_t e = hipFuncSetAttribute((const void*)hopf_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)bytes);
+    auto kern = lds ? (lpn == 4 ? hopf_kernel<true, 4> : hopf_kernel<true, 1>)
+                    : (lpn == 4 ? hopf_kernel<false, 4> : hopf_kernel<false, 1>);
+    if (bytes > 65536) {
+        hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
         if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
-        hipLaunchKernelGGL(hopf_kernel<true>, dim3(B), dim3(threads), bytes, st, p);
-    } else {
-        hipLaunchKernelGGL(hopf_kernel<false>, dim3(B), dim3(threads), bytes, st, p);
     }
+    hipLaunchKernelGGL(kern, dim3(B), dim3(threads), bytes, st, p);
     return wc_hip_check("wc_hopf_integrate");
 }
 

@@ -94,17 +94,23 @@ def fitting_measures(objective, dist_sim):
                      np.linalg.norm(objective - dist_sim), np.corrcoef(objective, dist_sim)[0, 1]])
 
 
-def update_sc(C, objective, dist_sim, epsilon, original_sum):
-    """optimize_SC_Hopf.py:89-101: homotopic step, clip, 30% density, total weight."""
+def update_sc(C, objective, dist_sim, epsilon, original_sum, threshold=0.3, lock_sum=True):
+    """optimize_SC_Hopf.py:89-101: homotopic step, clip, 30% density, total weight.
+
+    threshold=0 / lock_sum=False skip the two steps the reference marks optional
+    (:96); the shipped SC_opti_25julio.txt differs from the Deco SC only at the
+    homotopic entries, i.e. it was produced without them."""
     C = C.copy()
     h0, h1 = HOMOTOPIC[:, 0], HOMOTOPIC[:, 1]
     C[h0, h1] += graph_utils.matrix_recon(epsilon * (objective - dist_sim))[h0, h1]
     C[C < 0] = 0
-    C = graph_utils.thresholding(C, 0.3)
-    return C * original_sum / np.sum(C)
+    if threshold:
+        C = graph_utils.thresholding(C, threshold)
+    return C * original_sum / np.sum(C) if lock_sum else C
 
 
-def optimize(iters=100, seeds=10, epsilon=0.03, sc=None, empfc=None, device="cuda", log=None):
+def optimize(iters=100, seeds=10, epsilon=0.03, sc=None, empfc=None, device="cuda", log=None, threshold=0.3,
+             lock_sum=True):
     """The optimisation loop; returns (C, all_SCs [N][N][iters], fitting [4][iters])."""
     sc = datasets.load_deco_sc() if sc is None else np.asarray(sc, dtype=np.float64)
     empfc = datasets.load_empfc("W") if empfc is None else empfc
@@ -120,7 +126,7 @@ def optimize(iters=100, seeds=10, epsilon=0.03, sc=None, empfc=None, device="cud
         all_scs[:, :, i] = C
         dist_sim = graph_utils.get_uptri(simulated_fc(range(seeds), device))
         fitting[:, i] = fitting_measures(objective, dist_sim)
-        C = update_sc(C, objective, dist_sim, epsilon, original_sum)
+        C = update_sc(C, objective, dist_sim, epsilon, original_sum, threshold, lock_sum)
         HM.M = C
         HM.norm = np.mean(np.sum(HM.M, 0))
         if log:
@@ -134,11 +140,14 @@ def main(argv=None):
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--seeds", type=int, default=10)
     ap.add_argument("--epsilon", type=float, default=0.03)
+    ap.add_argument("--threshold", type=float, default=0.3, help="link density kept per iteration (0: skip)")
+    ap.add_argument("--no-lock-sum", action="store_true", help="skip the total-weight normalisation")
     ap.add_argument("--out", default="output")
     args = ap.parse_args(argv)
     os.makedirs(args.out, exist_ok=True)
     t0 = time.perf_counter()
-    C, all_scs, fitting = optimize(args.iters, args.seeds, args.epsilon, log=lambda d: print(json.dumps(d), flush=True))
+    C, all_scs, fitting = optimize(args.iters, args.seeds, args.epsilon, log=lambda d: print(json.dumps(d), flush=True),
+                                   threshold=args.threshold, lock_sum=not args.no_lock_sum)
     np.save(os.path.join(args.out, "all_SCs.npy"), all_scs)
     np.save(os.path.join(args.out, "fitting.npy"), fitting)
     np.savetxt(os.path.join(args.out, "SC_opti.txt"), C)
