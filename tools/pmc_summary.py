@@ -18,7 +18,7 @@ def summary(d, sub=None):
             k = r["Kernel_Name"]
             if sub and sub not in k:
                 continue
-            key = k.split("(")[0][-60:]
+            key = k.replace("void ", "").replace("(anonymous namespace)::", "").split("((")[0][:100]
             out[key][r["Counter_Name"]] += float(r["Counter_Value"])
             n[key].add(r.get("Dispatch_Id", r.get("Correlation_Id")))
     return {k: {c: v / max(1, len(n[k])) for c, v in cs.items()} | {"dispatches": len(n[k])} for k, cs in out.items()}
