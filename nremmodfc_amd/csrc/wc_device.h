@@ -210,3 +210,28 @@ template <> struct AccA<true> {
 
 
 }  // namespace wcdev
+
+namespace {
+// fp16 x3 coupling: CM scaled by sA = 2^(13 - e), max|CM| in [2^(e-1), 2^e), so every
+// |CM sA| < 2^14 (fp16 max 65504 with the 2^10-scaled E: products < 2^24).
+// scl[0] = sA, scl[1] = 1 / (2^10 sA) (folded into G by the kernel)
+__global__ void coupling_scale_kernel(const double* __restrict__ sc, int N, float* __restrict__ scl) {
+    __shared__ double red[256];
+    double m = 0.0;
+    for (size_t i = threadIdx.x; i < (size_t)N * N; i += 256) m = fmax(m, fabs(sc[i]));
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int e = 0;
+        if (red[0] > 0.0) frexp(red[0], &e);
+        e = max(-100, min(100, e));
+        scl[0] = ldexpf(1.0f, 13 - e);
+        scl[1] = ldexpf(1.0f, e - 23);
+    }
+}
+
+}  // namespace

@@ -116,28 +116,6 @@ __global__ void build_frag_bf16(const double* __restrict__ sc, int N, bf16x8* __
 // sized for the 3-part bf16 image)
 __host__ __device__ constexpr size_t hf_scale_offset(int NT) { return (size_t)NT * (NT / 2) * 2 * 64 * 16 / 4; }
 
-// fp16 x3 coupling: CM scaled by sA = 2^(13 - e), max|CM| in [2^(e-1), 2^e), so every
-// |CM sA| < 2^14 (fp16 max 65504 with the 2^10-scaled E: products < 2^24).
-// scl[0] = sA, scl[1] = 1 / (2^10 sA) (folded into G by the kernel)
-__global__ void coupling_scale_kernel(const double* __restrict__ sc, int N, float* __restrict__ scl) {
-    __shared__ double red[256];
-    double m = 0.0;
-    for (int i = threadIdx.x; i < N * N; i += 256) m = fmax(m, fabs(sc[i]));
-    red[threadIdx.x] = m;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        int e = 0;
-        if (red[0] > 0.0) frexp(red[0], &e);
-        e = max(-100, min(100, e));
-        scl[0] = ldexpf(1.0f, 13 - e);
-        scl[1] = ldexpf(1.0f, e - 23);
-    }
-}
-
 // fp16 x3: frag[((T*NC + c)*2 + p)*64 + lane][jj] = part p of CM[..] sA, hi = fp16(x),
 // lo = fp16(x - hi) (same element order as build_frag_bf16)
 template <int NT>

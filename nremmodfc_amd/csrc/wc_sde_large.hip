@@ -11,12 +11,12 @@
 //     (global_load_lds_dwordx4) into 2 LDS stages (48 KB, 3 workgroups per CU;
 //     3 stages at 2 workgroups per CU measured slower, as did prefetching the
 //     epilogue state into registers: tools/diag_large.py variants 104, 105);
-//   * fp32 product path: CM and E as three bf16 parts each, six cross terms on
-//     v_mfma_f32_16x16x32_bf16 (fp32-equivalent, as in wc_sde.hip).  CM's
-//     parts are pre-split in the A-operand image; E is kept ONLY as its exact
-//     3-way split (hi + mid + lo == E for fp32 E), written by the epilogue in
-//     the lane-linear order the DMA needs (xs_index), so the K loop is DMA +
-//     ds_read_b128 + MFMA with no VALU;
+//   * fp32 product path: CM sA and E 2^10 as two fp16 parts each (22-bit
+//     operands), three cross terms on v_mfma_f32_16x16x32_f16 with 1/(2^10 sA)
+//     folded into G -- the coupling of wc_sde.hip.  CM's parts are pre-split in
+//     the A-operand image; the epilogue writes E (fp32, tile-major) and its
+//     split in the lane-linear order the DMA needs (xs_index), so the K loop is
+//     DMA + ds_read_b128 + MFMA with no VALU;
 //   * fp64 parity path: v_mfma_f64_16x16x4_f64 on fp64 E;
 //   * the MFMA D fragment of a lane is 4 consecutive nodes of one simulation
 //     = exactly one Philox4x32-10 call (quad = node/4): the epilogue draws the
@@ -37,10 +37,11 @@ using namespace wcdev;
 typedef __attribute__((address_space(3))) void* lds_vptr;
 
 constexpr int kTile = 64;  // node and simulation padding unit (workgroup tile edge)
+constexpr int kParts = 2;  // fp16 parts per operand (hi, lo)
 
 struct Geo {
-    int B, N, Bp, Np, MT, NC, KC4;  // MT = Np/16 node tiles; NC = Np/32 bf16 chunks; KC4 = Np/4 f64 chunks
-    size_t o_frag, o_E, o_I, o_Ahi, o_Alo, o_G, o_S, o_X0, o_X1, total;
+    int B, N, Bp, Np, MT, NC, KC4;  // MT = Np/16 node tiles; NC = Np/32 fp16 chunks; KC4 = Np/4 f64 chunks
+    size_t o_frag, o_scl, o_E, o_I, o_Ahi, o_Alo, o_G, o_S, o_X0, o_X1, total;
 };
 
 size_t al(size_t x) { return (x + 255) & ~size_t(255); }
@@ -58,15 +59,16 @@ Geo geometry(int B, int N, int precision) {
     size_t o = 0;
     g.o_frag = o;
     if (precision == WC_F32) {
-        o += al((size_t)g.MT * g.NC * 3 * 64 * 16);
-        g.o_E = 0;  // E lives in the fp32 operand image X (exact: no separate copy)
+        o += al((size_t)g.MT * g.NC * kParts * 64 * 16);
+        g.o_scl = o; o += al(2 * sizeof(float));  // sA, 1 / (2^10 sA)
+        g.o_E = o; o += al(cells * 4);
         g.o_I = o; o += al(cells * 4);
         g.o_Ahi = o; o += al(cells * 4);
         g.o_Alo = o; o += al(cells * 4);
         g.o_G = o; o += al(cells * 4);
         g.o_S = o; o += al(cells * 4);
-        g.o_X0 = o; o += al(cells * 6);  // E as three bf16 parts in LDS-DMA order (xs_index)
-        g.o_X1 = o; o += al(cells * 6);
+        g.o_X0 = o; o += al(cells * 2 * kParts);  // E 2^10 as two fp16 parts in LDS-DMA order (xs_index)
+        g.o_X1 = o; o += al(cells * 2 * kParts);
     } else {
         o += al((size_t)g.MT * g.KC4 * 64 * 8);
         g.o_E = 0;
@@ -100,7 +102,7 @@ __host__ __device__ __forceinline__ size_t tm_index(const Geo& g, int b, int n) 
     return ((((size_t)(b >> 4) * g.MT + (n >> 4)) * 64 + lane) << 2) + (n & 3);
 }
 
-// bf16 B-operand image of E (three parts, exact: hi + mid + lo == E for fp32 E):
+// fp16 B-operand image of E 2^10 (two parts, hi + lo: 22 significant bits):
 // 16-B unit ((p*NC + c)*SB + b/64)*256 + g*64 + b%64 holds, for part p, k-chunk
 // c = n/32, node group g = (n%16)/4 and simulation b, the 8 values jj = 4h + r of
 // nodes 16(2c + h) + 4g + r -- lane (g, b%16)'s operand.  A workgroup's (p, c)
@@ -118,27 +120,27 @@ __host__ __device__ __forceinline__ size_t x64_index(const Geo& g, int b, int n)
 }
 
 // ---- A-operand images of CM ----
-__global__ void frag_bf16_kernel(const double* __restrict__ sc, Geo g, bf16x8* __restrict__ frag) {
+// CM sA as two fp16 parts (hi = fp16(x), lo = fp16(x - hi)), sA from coupling_scale_kernel
+__global__ void frag_f16_kernel(const double* __restrict__ sc, Geo g, const float* __restrict__ scl,
+                                f16x8* __restrict__ frag) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // ((m*NC + c)*64 + lane)
     if (idx >= g.MT * g.NC * 64) return;
     const int lane = idx & 63;
     const int mc = idx >> 6;
     const int m = mc / g.NC, c = mc % g.NC;
     const int row = 16 * m + (lane & 15);
-    bf16x8 part[3];
+    const double sA = scl[0];
+    f16x8 part[kParts];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
         const int col = 16 * (2 * c + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);
-        const double x = (row < g.N && col < g.N) ? sc[(size_t)row * g.N + col] : 0.0;
-        const __bf16 h = (__bf16)(float)x;
-        const double r1 = x - (double)(float)h;
-        const __bf16 mm = (__bf16)(float)r1;
+        const double x = (row < g.N && col < g.N) ? sc[(size_t)row * g.N + col] * sA : 0.0;
+        const _Float16 h = (_Float16)(float)x;
         part[0][jj] = h;
-        part[1][jj] = mm;
-        part[2][jj] = (__bf16)(float)(r1 - (double)(float)mm);
+        part[1][jj] = (_Float16)(float)(x - (double)(float)h);
     }
 #pragma unroll
-    for (int p = 0; p < 3; ++p) frag[((size_t)mc * 3 + p) * 64 + lane] = part[p];
+    for (int p = 0; p < kParts; ++p) frag[((size_t)mc * kParts + p) * 64 + lane] = part[p];
 }
 
 __global__ void frag_f64_kernel(const double* __restrict__ sc, Geo g, double* __restrict__ frag) {
@@ -168,19 +170,20 @@ __global__ void prep_kernel(LArgs a, const double* __restrict__ G, const double*
     if constexpr (sizeof(Real) == 4) {
         {
             float v[4] = {(float)e, 0.f, 0.f, 0.f};
-            bf16x4 h, m, l;
-            split3(v, h, m, l);
-            __bf16* X = reinterpret_cast<__bf16*>(a.ws + g.o_X0);
+            f16x4 h, l;
+            split2h(v, h, l);
+            _Float16* X = reinterpret_cast<_Float16*>(a.ws + g.o_X0);
             X[xs_index(g, 0, b, n)] = h[0];
-            X[xs_index(g, 1, b, n)] = m[0];
-            X[xs_index(g, 2, b, n)] = l[0];
+            X[xs_index(g, 1, b, n)] = l[0];
         }
+        reinterpret_cast<float*>(a.ws + g.o_E)[t] = (float)e;
         reinterpret_cast<float*>(a.ws + g.o_I)[t] = (float)in;
         AccA<true> acc;
         acc.set(ai);
         reinterpret_cast<float*>(a.ws + g.o_Ahi)[t] = acc.hi;
         reinterpret_cast<float*>(a.ws + g.o_Alo)[t] = acc.lo;
-        reinterpret_cast<float*>(a.ws + g.o_G)[t] = (float)gc;
+        // the MFMA sums (CM sA)(E 2^10): 1 / (2^10 sA) is folded into G (a power of two: exact)
+        reinterpret_cast<float*>(a.ws + g.o_G)[t] = (float)gc * reinterpret_cast<const float*>(a.ws + g.o_scl)[1];
         reinterpret_cast<float*>(a.ws + g.o_S)[t] = Tr<float>::slope(s);
     } else {
         reinterpret_cast<double*>(a.ws + g.o_I)[t] = in;
@@ -200,8 +203,8 @@ __global__ void finish_kernel(LArgs a, int buf, double* __restrict__ E, double* 
     const int b = (int)(idx / g.N), n = (int)(idx % g.N);
     const size_t t = tm_index(g, b, n);
     if constexpr (sizeof(Real) == 4) {
-        const __bf16* X = reinterpret_cast<const __bf16*>(a.ws + (buf ? g.o_X1 : g.o_X0));
-        E[idx] = ((float)X[xs_index(g, 0, b, n)] + (float)X[xs_index(g, 1, b, n)]) + (float)X[xs_index(g, 2, b, n)];
+        (void)buf;
+        E[idx] = reinterpret_cast<const float*>(a.ws + g.o_E)[t];
         I[idx] = reinterpret_cast<const float*>(a.ws + g.o_I)[t];
         A[idx] = (double)reinterpret_cast<const float*>(a.ws + g.o_Ahi)[t] +
                  (double)reinterpret_cast<const float*>(a.ws + g.o_Alo)[t];
@@ -268,33 +271,35 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
 
     if constexpr (sizeof(Real) == 4) {
         // K loop fed by LDS-DMA: each 32-node k-chunk of the workgroup's A rows
-        // (4 tiles x 3 parts, pre-split image) and E columns (3 parts x 64 sims,
-        // pre-split by the previous step's epilogue) is 24 x 1 KB lane-linear
-        // global_load_lds_dwordx4 into a ring of STAGES LDS stages (6 per wave),
+        // (4 tiles x 2 fp16 parts, pre-split image) and E columns (2 parts x 64
+        // sims, split by the previous step's epilogue) is 16 x 1 KB lane-linear
+        // global_load_lds_dwordx4 into a ring of STAGES LDS stages (4 per wave),
         // STAGES-1 chunks in flight; a counted vmcnt + raw s_barrier retire a stage.
         // The loop body is then only ds_read_b128 + MFMA (no VALU staging).
-        __shared__ bf16x8 lds[STAGES][2][12 * 64];  // [stage][A | B][unit][lane]
-        const bf16x8* F = reinterpret_cast<const bf16x8*>(a.ws + g.o_frag);
-        const bf16x8* X = reinterpret_cast<const bf16x8*>(a.ws + (buf ? g.o_X1 : g.o_X0));
+        constexpr int kU = 2;  // A units and B units per wave per chunk
+        __shared__ f16x8 lds[STAGES][2][4 * kParts * 64];  // [stage][A | B][unit][lane]
+        const f16x8* F = reinterpret_cast<const f16x8*>(a.ws + g.o_frag);
+        const f16x8* X = reinterpret_cast<const f16x8*>(a.ws + (buf ? g.o_X1 : g.o_X0));
         const int SB = g.Bp / kTile;
-        // this wave's 3 A units (tile ta, part pa) and 3 B units (part pb, group gb)
-        const bf16x8* asrc[3];
-        const bf16x8* bsrc[3];
-        int aoff[3], boff[3];
+        // this wave's A units (tile ta, part pa) and B units (part pb, group gb)
+        const f16x8* asrc[kU];
+        const f16x8* bsrc[kU];
+        int aoff[kU], boff[kU];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int ua = 3 * w + i, ta = ua / 3, pa = ua % 3;
-            asrc[i] = F + ((size_t)(mb * 4 + ta) * g.NC * 3 + pa) * 64 + lane;  // + c * 192
-            aoff[i] = (ta * 3 + pa) * 64;
-            const int ub = 3 * w + i, pb = ub / 4, gb = ub % 4;
+        for (int i = 0; i < kU; ++i) {
+            const int ua = kU * w + i, ta = ua / kParts, pa = ua % kParts;
+            asrc[i] = F + ((size_t)(mb * 4 + ta) * g.NC * kParts + pa) * 64 + lane;  // + c * kParts * 64
+            aoff[i] = (ta * kParts + pa) * 64;
+            const int ub = kU * w + i, pb = ub / 4, gb = ub % 4;
             bsrc[i] = X + (((size_t)pb * g.NC * SB + sb) * 256 + gb * 64) + lane;  // + c * SB * 256
             boff[i] = (pb * 4 + gb) * 64;
         }
         const size_t bstep = (size_t)SB * 256;
         auto issue = [&](int c, int st) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                __builtin_amdgcn_global_load_lds(asrc[i] + (size_t)c * 192, (lds_vptr)(&lds[st][0][aoff[i]]), 16, 0, 0);
+            for (int i = 0; i < kU; ++i) {
+                __builtin_amdgcn_global_load_lds(asrc[i] + (size_t)c * kParts * 64, (lds_vptr)(&lds[st][0][aoff[i]]), 16,
+                                                 0, 0);
                 __builtin_amdgcn_global_load_lds(bsrc[i] + (size_t)c * bstep, (lds_vptr)(&lds[st][1][boff[i]]), 16, 0, 0);
             }
         };
@@ -309,19 +314,19 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             if (DIAG == 1 || c + STAGES - 2 >= g.NC) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             } else if constexpr (STAGES == 3) {
-                asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // the younger chunk's 2 kU loads
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             if (DIAG != 1 && c + STAGES - 1 < g.NC) issue(c + STAGES - 1, (c + STAGES - 1) % STAGES);
-            bf16x8 fa[2][3], fb[2][3];
+            f16x8 fa[2][kParts], fb[2][kParts];
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    fa[u][p] = lds[DIAG == 1 ? 0 : st][0][((ua + u) * 3 + p) * 64 + lane];
+                for (int p = 0; p < kParts; ++p) {
+                    fa[u][p] = lds[DIAG == 1 ? 0 : st][0][((ua + u) * kParts + p) * 64 + lane];
                     fb[u][p] = lds[DIAG == 1 ? 0 : st][1][(p * 4 + gq) * 64 + 16 * (ub + u) + j];
                 }
 #pragma unroll
@@ -332,13 +337,10 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
                         acc[u][v][0] += (float)fa[u][0][0] * (float)fb[v][0][0];
                         continue;
                     }
-                    // small terms first (2^-18, 2^-9, 1), as in wc_sde.hip
-                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][2], fb[v][0], acc[u][v], 0, 0, 0);
-                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[v][1], acc[u][v], 0, 0, 0);
-                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][2], acc[u][v], 0, 0, 0);
-                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[v][0], acc[u][v], 0, 0, 0);
-                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][1], acc[u][v], 0, 0, 0);
-                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[v][0], acc[u][v], 0, 0, 0);
+                    // small terms first (2^-11: lo.hi, hi.lo; 1: hi.hi), as in wc_sde.hip
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[u][1], fb[v][0], acc[u][v], 0, 0, 0);
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[u][0], fb[v][1], acc[u][v], 0, 0, 0);
+                    acc[u][v] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[u][0], fb[v][0], acc[u][v], 0, 0, 0);
                 }
         }
     } else {
@@ -387,12 +389,8 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             AccA<sizeof(Real) == 4> Av[4];
             real4* Xn;  // next step's E image (f64) / tile-major E (f32)
             if constexpr (sizeof(Real) == 4) {
-                // E = hi + mid + lo (exact) of this lane's 4 nodes: 8 B per part
-                const bf16x4* Xc = reinterpret_cast<const bf16x4*>(a.ws + (buf ? g.o_X1 : g.o_X0));
-                const bf16x4 eh = Xc[xs_index(g, 0, b, n0) >> 2], em = Xc[xs_index(g, 1, b, n0) >> 2],
-                             el = Xc[xs_index(g, 2, b, n0) >> 2];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) Ev[r] = ((float)eh[r] + (float)em[r]) + (float)el[r];
+                // E of this lane's 4 nodes (fp32 state, tile-major like I)
+                Ev = kState ? reinterpret_cast<const real4*>(a.ws + g.o_E)[t4] : real4{0.1, 0.1, 0.1, 0.1};
                 Xn = nullptr;
                 real4 hi, lo;
                 if constexpr (kPF) {
@@ -452,14 +450,15 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             }
             if (kState) Iw[t4] = In;
             if constexpr (sizeof(Real) == 4) {
-                // next step's B operand: the exact 3-way split of the new E
+                // next step's B operand: the fp16 split of the new E 2^10
                 float ev[4] = {En[0], En[1], En[2], En[3]};
-                bf16x4 ph[3];
-                split3(ev, ph[0], ph[1], ph[2]);
-                bf16x4* Xo = reinterpret_cast<bf16x4*>(a.ws + (buf ? g.o_X0 : g.o_X1));
+                f16x4 ph[kParts];
+                split2h(ev, ph[0], ph[1]);
+                f16x4* Xo = reinterpret_cast<f16x4*>(a.ws + (buf ? g.o_X0 : g.o_X1));
 #pragma unroll
-                for (int p = 0; p < 3; ++p) Xo[xs_index(g, p, b, n0) >> 2] = ph[p];
+                for (int p = 0; p < kParts; ++p) Xo[xs_index(g, p, b, n0) >> 2] = ph[p];
                 if (!kState) continue;
+                reinterpret_cast<real4*>(a.ws + g.o_E)[t4] = En;
                 real4 hi, lo;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -494,8 +493,10 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
     const Geo& g = a.g;
     if constexpr (sizeof(Real) == 4) {
         const int n = g.MT * g.NC * 64;
-        hipLaunchKernelGGL(frag_bf16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc, g,
-                           reinterpret_cast<bf16x8*>(a.ws + g.o_frag));
+        float* scl = reinterpret_cast<float*>(a.ws + g.o_scl);
+        hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(256), 0, st, sc, N, scl);
+        hipLaunchKernelGGL(frag_f16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc, g, scl,
+                           reinterpret_cast<f16x8*>(a.ws + g.o_frag));
     } else {
         const int n = g.MT * g.KC4 * 64;
         hipLaunchKernelGGL(frag_f64_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc, g,
@@ -550,6 +551,8 @@ int wc_large_diag(int variant, const wc_params* p, int B, int N, const double* s
                                                       0, 0, nullptr, nullptr, nullptr, workspace, st);
         case 105: return run_large<float, 0, 2, true>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip,
                                                       0, 0, nullptr, nullptr, nullptr, workspace, st);
+        case 106: return run_large<float, 0, 3, false>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip,
+                                                       0, 0, nullptr, nullptr, nullptr, workspace, st);
         default: return wc_set_err(WC_EINVAL, "unknown large-N diagnostic variant");
     }
 }

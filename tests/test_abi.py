@@ -34,9 +34,10 @@ def test_abi_version_and_workspace():
     assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16   # bf16x6 image
     assert L.wc_workspace_size(20000, 90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
     assert L.wc_workspace_size(1, 16, _lib.WC_F32) == 2 * 1 * 3 * 64 * 16
-    # N > 96 (wc_sde_large.hip): bf16x3 A image + 5 fp32 state arrays (I, a_ie pair, G, slope) + 2 bf16x3 E images
+    # N > 96 (wc_sde_large.hip): fp16x2 A image + 2 scale floats (one 256-B slot) + 6 fp32 state arrays
+    # (E, I, a_ie pair, G, slope) + 2 fp16x2 E operand images
     Bp, Np = 2560, 1024
-    want = (Np // 16) * (Np // 32) * 3 * 64 * 16 + Bp * Np * (5 * 4 + 2 * 6)
+    want = (Np // 16) * (Np // 32) * 2 * 64 * 16 + 256 + Bp * Np * (6 * 4 + 2 * 4)
     assert L.wc_workspace_size(2500, 1000, _lib.WC_F32) == want
     assert L.wc_workspace_size(2500, 1000, _lib.WC_F64) == (Np // 16) * (Np // 4) * 64 * 8 + Bp * Np * 6 * 8
 
