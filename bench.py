@@ -191,6 +191,7 @@ def main():
     per_launch_ns = B * N * EULER
     achieved = per_launch_ns * fl / (kern["sde"] * 1e-3) / 1e12
     traffic = None
+    util = {}
     pmc = os.path.join(ROOT, "profiles", "pmc_sde.json")
     if os.path.exists(pmc):
         try:
@@ -198,6 +199,8 @@ def main():
             if d.get("B") == B and d.get("N") == N and d.get("euler_steps") == EULER and \
                     d.get("precision") == args.precision:
                 traffic = d.get("hbm_bytes_per_launch")
+                util = {k: d[k] for k in ("valu_insts_per_wave_step", "mfma_insts_per_wave_step", "mfma_busy_frac")
+                        if k in d}
         except (ValueError, OSError):
             traffic = None
     out = {
@@ -229,7 +232,8 @@ def main():
                      "kernel": ("wc_sde_kernel (one launch = %d Euler steps of %d sims)" % (EULER, B) if N <= 96 else
                                 "step_kernel (wc_sde_large.hip; %d launches of 1 Euler step, %d sims)" % (EULER, B)),
                      "kernel_ms_per_launch": kern["sde"],
-                     "flops_per_node_step": fl},
+                     "flops_per_node_step": fl,
+                     "pmc": util or None},
         "kernel_ms": kern,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
