@@ -46,7 +46,10 @@ d = {"kernel": kf, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
              "(16 simulations x 2 node tiles of 16; 3 waves per group of 16 simulations). mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / "
              "(GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)."}
 json.dump(d, open("profiles/pmc_sde.json", "w"), indent=1)
+json.dump(d, open("gpurun_out/prof/pmc_sde.json", "w"), indent=1)  # gpurun merges gpurun_out/ back only
 print(json.dumps(d))
 PY
 cp $OUT/bench_kernel_stats.csv profiles/r01_bench_kernel_stats.csv 2>/dev/null || true
+# on the GPU box only gpurun_out/ travels back: copy gpurun_out/prof/pmc_sde.json and
+# gpurun_out/prof/bench_kernel_stats.csv into profiles/ afterwards
 tail -1 $OUT/trace.log
