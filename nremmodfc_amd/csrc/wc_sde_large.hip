@@ -41,7 +41,7 @@ constexpr int kParts = 2;  // fp16 parts per operand (hi, lo)
 
 struct Geo {
     int B, N, Bp, Np, MT, NC, KC4;  // MT = Np/16 node tiles; NC = Np/32 fp16 chunks; KC4 = Np/4 f64 chunks
-    size_t o_frag, o_scl, o_E, o_I, o_Ahi, o_Alo, o_G, o_S, o_X0, o_X1, total;
+    size_t o_frag, o_scl, o_E, o_I, o_Ahi, o_Alo, o_G, o_S, o_X0, o_X1, o_GS1, o_uni, total;
 };
 
 size_t al(size_t x) { return (x + 255) & ~size_t(255); }
@@ -69,6 +69,8 @@ Geo geometry(int B, int N, int precision) {
         g.o_S = o; o += al(cells * 4);
         g.o_X0 = o; o += al(cells * 2 * kParts);  // E 2^10 as two fp16 parts in LDS-DMA order (xs_index)
         g.o_X1 = o; o += al(cells * 2 * kParts);
+        g.o_GS1 = o; o += al((size_t)g.Bp * 8);  // per-simulation (G scaled, slope) when they do not vary by node
+        g.o_uni = o; o += al(sizeof(uint32_t));   // 1: every simulation's G and sigmaE are node-independent
     } else {
         o += al((size_t)g.MT * g.KC4 * 64 * 8);
         g.o_E = 0;
@@ -192,6 +194,22 @@ __global__ void prep_kernel(LArgs a, const double* __restrict__ G, const double*
         reinterpret_cast<double*>(a.ws + g.o_S)[t] = s;
         reinterpret_cast<double*>(a.ws + g.o_X0)[x64_index(g, b, n)] = e;
     }
+}
+
+// homogeneous sweeps (whole_sweep_both.py) give every node of a simulation the same G and
+// sigmaE: then the epilogue reads one (G, slope) pair per simulation instead of two
+// per-cell images (8 of its 44 B of state per node-step).  uni starts at 1 (set by the
+// host-side memset) and any node that differs from node 0 of its simulation clears it.
+__global__ void uniform_params_kernel(LArgs a, const double* __restrict__ G, const double* __restrict__ sigmaE) {
+    const Geo& g = a.g;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)g.B * g.N) return;
+    const int b = (int)(idx / g.N);
+    const size_t o0 = (size_t)b * g.N;
+    if (G[idx] != G[o0] || sigmaE[idx] != sigmaE[o0]) atomicAnd(reinterpret_cast<uint32_t*>(a.ws + g.o_uni), 0u);
+    if (idx == o0)
+        reinterpret_cast<float2*>(a.ws + g.o_GS1)[b] =
+            make_float2((float)G[o0] * reinterpret_cast<const float*>(a.ws + g.o_scl)[1], Tr<float>::slope(sigmaE[o0]));
 }
 
 template <typename Real>
@@ -368,6 +386,7 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
     const Real dt = (Real)a.dtSim, tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;
     const uint64_t gstep = (uint64_t)(a.step0 + s);
     const size_t BN = (size_t)g.B * g.N;
+    const bool uni = sizeof(Real) == 4 && __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(a.ws + g.o_uni));
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int b = 16 * (s0 + v) + j;
@@ -381,8 +400,16 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             real4* Iw = reinterpret_cast<real4*>(a.ws + g.o_I);
             real4* Ahw = reinterpret_cast<real4*>(a.ws + g.o_Ahi);
             constexpr bool kState = DIAG != 3;
-            const real4 Gv = kState ? reinterpret_cast<const real4*>(a.ws + g.o_G)[t4] : real4{0.16, 0.16, 0.16, 0.16};
-            const real4 Sv = kState ? reinterpret_cast<const real4*>(a.ws + g.o_S)[t4] : real4{11, 11, 11, 11};
+            real4 Gv, Sv;
+            if (sizeof(Real) == 4 && uni) {  // one (G, slope) per simulation (uniform_params_kernel)
+                const float2 gs = kState ? reinterpret_cast<const float2*>(a.ws + g.o_GS1)[live ? b : g.B - 1]
+                                         : make_float2(0.16f, 11.f);
+                Gv = real4{gs.x, gs.x, gs.x, gs.x};
+                Sv = real4{gs.y, gs.y, gs.y, gs.y};
+            } else {
+                Gv = kState ? reinterpret_cast<const real4*>(a.ws + g.o_G)[t4] : real4{0.16, 0.16, 0.16, 0.16};
+                Sv = kState ? reinterpret_cast<const real4*>(a.ws + g.o_S)[t4] : real4{11, 11, 11, 11};
+            }
             real4 Ev, Iv;
             if constexpr (kPF) Iv = pfI[v][u];
             else Iv = kState ? Iw[t4] : real4{0.1, 0.1, 0.1, 0.1};
@@ -505,6 +532,12 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
     const size_t cells = (size_t)g.Bp * g.Np;
     hipLaunchKernelGGL(prep_kernel<Real>, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, a, G, sigmaE, E,
                        I, A);
+    if constexpr (sizeof(Real) == 4) {
+        hipError_t me = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(a.ws + g.o_uni), 1, 1, st);
+        if (me != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(me));
+        const size_t bn = (size_t)B * N;
+        hipLaunchKernelGGL(uniform_params_kernel, dim3((unsigned)((bn + 255) / 256)), dim3(256), 0, st, a, G, sigmaE);
+    }
     const int W = (g.Bp / kTile) * (g.Np / kTile);
     for (int64_t s = 0; s < nsteps; ++s) {
         const int rec_row = (rec_every > 0 && s % rec_every == 0) ? (int)(s / rec_every) : -1;

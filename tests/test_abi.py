@@ -37,7 +37,8 @@ def test_abi_version_and_workspace():
     # N > 96 (wc_sde_large.hip): fp16x2 A image + 2 scale floats (one 256-B slot) + 6 fp32 state arrays
     # (E, I, a_ie pair, G, slope) + 2 fp16x2 E operand images
     Bp, Np = 2560, 1024
-    want = (Np // 16) * (Np // 32) * 2 * 64 * 16 + 256 + Bp * Np * (6 * 4 + 2 * 4)
+    # + per-simulation (G, slope) pairs and the uniformity flag (one 256-B slot)
+    want = (Np // 16) * (Np // 32) * 2 * 64 * 16 + 256 + Bp * Np * (6 * 4 + 2 * 4) + Bp * 8 + 256
     assert L.wc_workspace_size(2500, 1000, _lib.WC_F32) == want
     assert L.wc_workspace_size(2500, 1000, _lib.WC_F64) == (Np // 16) * (Np // 4) * 64 * 8 + Bp * Np * 6 * 8
 
