@@ -171,7 +171,8 @@ int wc_hma(int B, int N, double* fc, double* hin, double* hse, double* hin_node,
  * s % rec_every == 0 is stored at rec[s / rec_every][B][N] (and y at rec_y,
  * which may be NULL): a run recorded from its first step gives the
  * reference's results[k] = state after k*downsamp steps (:140-149).  M is N x N
- * (row i = inputs of node i); workspace >= wc_hopf_workspace_size(N). */
+ * (row i = inputs of node i); workspace >= wc_hopf_workspace_size(B, N): the
+ * weight image and one segment (512 steps) of pre-generated normals. */
 typedef struct wc_hopf_params {
     double a;     /* bifurcation parameter (Hopf_model_multi.py:22) */
     double w;     /* angular frequency, 0.05 * 2 pi (:23) */
@@ -181,7 +182,7 @@ typedef struct wc_hopf_params {
     double norm;  /* mean column sum of M (:37, optimize_SC_Hopf.py:30,101) */
 } wc_hopf_params;
 
-size_t wc_hopf_workspace_size(int N);
+size_t wc_hopf_workspace_size(int B, int N);
 int wc_hopf_integrate(const wc_hopf_params* p, int B, int N, const double* M, const uint64_t* keys,
                       double* x, double* y, int64_t step0, int64_t nsteps, int64_t rec_every,
                       double* rec, double* rec_y, void* workspace, size_t ws_bytes, void* stream);

@@ -118,7 +118,7 @@ def sim_batch(seeds, want_y=False, device="cuda"):
     x = torch.from_numpy(np.stack([c[0] for c in ics])).to(device)
     y = torch.from_numpy(np.stack([c[1] for c in ics])).to(device)
     keys = torch.tensor(seeds, dtype=torch.int64, device=device)
-    ws = torch.empty(L.wc_hopf_workspace_size(n) // 8 + 1, dtype=torch.float64, device=device)
+    ws = torch.empty(L.wc_hopf_workspace_size(B, n) // 8 + 1, dtype=torch.float64, device=device)
     rx = torch.empty((nmax, B, n), dtype=torch.float64, device=device)
     ry = torch.empty_like(rx) if want_y else None
     hp = _params()

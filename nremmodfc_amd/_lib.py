@@ -63,7 +63,7 @@ _SIGNATURES = {
     "wc_fc_metrics": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wc_kuramoto": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "wc_hma": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "wc_hopf_workspace_size": (c_sz, [c_int]),
+    "wc_hopf_workspace_size": (c_sz, [c_int, c_int]),
     "wc_hopf_integrate": (c_int, [ctypes.POINTER(WCHopfParamsC), c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                   c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "wc_filtfilt": (c_int, [c_int, ctypes.POINTER(c_dbl), ctypes.POINTER(c_dbl), ctypes.POINTER(c_dbl),

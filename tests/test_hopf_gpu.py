@@ -22,12 +22,12 @@ def _dev_hopf(params, M, keys, x, y, step0, nsteps, rec_every=0, want_y=False):
     tx, ty = torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda()
     m = torch.from_numpy(np.ascontiguousarray(M)).cuda()
     k = torch.tensor(list(keys), dtype=torch.int64, device="cuda")
-    ws = torch.empty(N * N, dtype=torch.float64, device="cuda")
+    ws = torch.empty(L.wc_hopf_workspace_size(B, N) // 8 + 1, dtype=torch.float64, device="cuda")
     n_rec = -(-nsteps // rec_every) if rec_every else 0
     rec = torch.empty((n_rec, B, N), dtype=torch.float64, device="cuda") if rec_every else None
     recy = torch.empty_like(rec) if (rec_every and want_y) else None
     rc = L.wc_hopf_integrate(ctypes.byref(hp), B, N, _lib.ptr(m), _lib.ptr(k), _lib.ptr(tx), _lib.ptr(ty), step0,
-                             nsteps, rec_every, _lib.ptr(rec), _lib.ptr(recy), _lib.ptr(ws), N * N * 8,
+                             nsteps, rec_every, _lib.ptr(rec), _lib.ptr(recy), _lib.ptr(ws), ws.numel() * 8,
                              _lib.stream_handle())
     _lib.check(rc, "wc_hopf_integrate")
     torch.cuda.synchronize()
@@ -49,6 +49,19 @@ def test_hopf_matches_oracle(cuda, N, B, G):
     orec = oracle.hopf_integrate(p, M, keys, ox, oy, 17, 1500, 3)
     assert np.abs(grec.transpose(1, 0, 2) - orec).max() < 1e-10
     assert np.abs(gx - ox).max() < 1e-10 and np.abs(gy - oy).max() < 1e-10
+
+
+def test_hopf_records_across_noise_segments(cuda):
+    """Records with a period that does not divide the 512-step noise segments land on the right rows."""
+    M = datasets.load_deco_sc()[:20, :20]
+    p = dict(a=0.0, w=0.3, beta=0.05, dt=0.1, G=0.6, norm=np.mean(M.sum(0)))
+    x0, y0 = np.full((2, 20), 0.3), np.full((2, 20), 0.1)
+    gx, gy, grec, grecy = _dev_hopf(p, M, [1, 2], x0.copy(), y0.copy(), 3, 1301, 7, want_y=True)
+    ox, oy = x0.copy(), y0.copy()
+    orec = oracle.hopf_integrate(p, M, [1, 2], ox, oy, 3, 1301, 7)
+    assert grec.shape[0] == orec.shape[1] == 186
+    assert np.abs(grec.transpose(1, 0, 2) - orec).max() < 1e-10
+    assert np.abs(gx - ox).max() < 1e-10
 
 
 def test_hopf_chunking_is_exact(cuda):
