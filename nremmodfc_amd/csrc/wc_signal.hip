@@ -577,6 +577,7 @@ __global__ void hilbert_kernel_q(int M, double* q) {
 
 // ---------------- per-simulation FC, goodness of fit, mean, Kuramoto ----------------
 constexpr int kFcThreads = 256;
+constexpr int kMaxN = 96;  // wc_fc_metrics: N <= 96
 
 __device__ double block_sum(double v, double* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -641,10 +642,10 @@ struct FcArgs {
 // LDS: fc[N*N] | emp[N*N] (also the time-chunk staging area before emp is loaded) | red[8]
 __global__ void __launch_bounds__(kFcThreads) fc_metrics_kernel(const FcArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int N = a.N, M = a.M, NN = N * N;
+    const int N = a.N, M = a.M, NN = N * N, NN2 = (NN + 1) & ~1;  // NN2: 16-B aligned areas
     double* fc = lds;
-    double* emp = lds + NN;
-    double* red = lds + 2 * NN;
+    double* emp = lds + NN2;
+    double* red = emp + NN2;
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const int64_t C = (int64_t)a.B * N;
@@ -655,55 +656,85 @@ __global__ void __launch_bounds__(kFcThreads) fc_metrics_kernel(const FcArgs a) 
         __syncthreads();
     } else {
     // ---- np.cov: node means, centred cross products, 1/(M-1) ----
-    double* mean = red + 8;  // [N] after red
-    for (int n = tid; n < N; n += blockDim.x) {
-        double s = 0;
-        for (int t = 0; t < M; ++t) s += xb[(int64_t)t * C + n];
-        mean[n] = s / M;
+    // means: S = kFcThreads / N slices per node (t = h, h + S, ...), combined in slice order
+    double* mean = red + 8;        // [N] after red
+    double* msl = mean + kMaxN;    // [S][N] slice sums
+    const int S = kFcThreads / N;
+    if (tid < S * N) {
+        const int n = tid % N, h = tid / N;
+        double sm = 0;
+        for (int t = h; t < M; t += S) sm += xb[(int64_t)t * C + n];
+        msl[h * N + n] = sm;
     }
     __syncthreads();
-    // pairs (i <= j) distributed over threads; time staged through LDS (emp area)
-    const int npairs = N * (N + 1) / 2;
-    constexpr int kMaxPairs = (96 * 97 / 2 + kFcThreads - 1) / kFcThreads;
-    double acc[kMaxPairs];
+    for (int n = tid; n < N; n += blockDim.x) {
+        double sm = 0;
+        for (int h = 0; h < S; ++h) sm += msl[h * N + n];
+        mean[n] = sm / M;
+    }
+    __syncthreads();
+    // cross products as 4 x 4 register tiles of the (padded) upper triangle: per sample
+    // a tile reads 2 x 4 centred values (4 ds_read_b128) for 16 FMAs; every (i, j) still
+    // sums its samples in time order.  Time is staged through LDS (emp area).
+    const int Np = (N + 3) & ~3, NB = Np / 4;
+    const int ntiles = NB * (NB + 1) / 2;
+    constexpr int kMaxTiles = ((kMaxN / 4) * (kMaxN / 4 + 1) / 2 + kFcThreads - 1) / kFcThreads;  // 2
+    double acc[kMaxTiles][4][4];
+    int ti[kMaxTiles], tj[kMaxTiles];
 #pragma unroll
-    for (int k = 0; k < kMaxPairs; ++k) acc[k] = 0.0;
-    const int TCH = NN / N;  // time samples per staging chunk (N*N doubles of room)
+    for (int k = 0; k < kMaxTiles; ++k) {
+        const int p = min(tid + k * kFcThreads, ntiles - 1);
+        // p -> (bi, bj), bi <= bj, row-major over the upper triangle of NB x NB blocks
+        int bi = (int)((2 * NB + 1 - sqrt((double)(2 * NB + 1) * (2 * NB + 1) - 8.0 * p)) / 2);
+        while (bi > 0 && bi * (2 * NB - bi + 1) / 2 > p) --bi;
+        while ((bi + 1) * (2 * NB - bi) / 2 <= p) ++bi;
+        ti[k] = 4 * bi;
+        tj[k] = 4 * (bi + (p - bi * (2 * NB - bi + 1) / 2));
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[k][r][q] = 0.0;
+    }
+    const int TCH = NN / Np;  // time samples per staging chunk (N*N doubles of room)
     for (int t0 = 0; t0 < M; t0 += TCH) {
         const int tn = min(TCH, M - t0);
-        for (int i = tid; i < tn * N; i += blockDim.x) {
-            const int tt = i / N, n = i % N;
-            emp[i] = xb[(int64_t)(t0 + tt) * C + n] - mean[n];
+        for (int i = tid; i < tn * Np; i += blockDim.x) {
+            const int tt = i / Np, n = i % Np;
+            emp[i] = n < N ? xb[(int64_t)(t0 + tt) * C + n] - mean[n] : 0.0;
         }
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kMaxPairs; ++k) {
-            const int p = tid + k * kFcThreads;
-            if (p < npairs) {
-                // p -> (i, j), i <= j, row-major over the upper triangle
-                int i = (int)((2 * N + 1 - sqrt((double)(2 * N + 1) * (2 * N + 1) - 8.0 * p)) / 2);
-                while (i > 0 && i * (2 * N - i + 1) / 2 > p) --i;
-                while ((i + 1) * (2 * N - i) / 2 <= p) ++i;
-                const int j = i + (p - i * (2 * N - i + 1) / 2);
-                double s = acc[k];
-                for (int tt = 0; tt < tn; ++tt) s += emp[tt * N + i] * emp[tt * N + j];
-                acc[k] = s;
+        for (int k = 0; k < kMaxTiles; ++k) {
+            if (tid + k * kFcThreads < ntiles) {
+                for (int tt = 0; tt < tn; ++tt) {
+                    const double2* row = reinterpret_cast<const double2*>(emp + tt * Np);
+                    const double2 a0 = row[ti[k] / 2], a1 = row[ti[k] / 2 + 1];
+                    const double2 b0 = row[tj[k] / 2], b1 = row[tj[k] / 2 + 1];
+                    const double xi[4] = {a0.x, a0.y, a1.x, a1.y}, xj[4] = {b0.x, b0.y, b1.x, b1.y};
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) acc[k][r][q] += xi[r] * xj[q];
+                }
             }
         }
         __syncthreads();
     }
     const double fact = 1.0 / (M - 1);
 #pragma unroll
-    for (int k = 0; k < kMaxPairs; ++k) {
-        const int p = tid + k * kFcThreads;
-        if (p < npairs) {
-            int i = (int)((2 * N + 1 - sqrt((double)(2 * N + 1) * (2 * N + 1) - 8.0 * p)) / 2);
-            while (i > 0 && i * (2 * N - i + 1) / 2 > p) --i;
-            while ((i + 1) * (2 * N - i) / 2 <= p) ++i;
-            const int j = i + (p - i * (2 * N - i + 1) / 2);
-            const double cv = acc[k] * fact;
-            fc[i * N + j] = cv;
-            fc[j * N + i] = cv;
+    for (int k = 0; k < kMaxTiles; ++k) {
+        if (tid + k * kFcThreads < ntiles) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int i = ti[k] + r, j = tj[k] + q;
+                    if (i < N && j < N && i <= j) {
+                        const double cv = acc[k][r][q] * fact;
+                        fc[i * N + j] = cv;
+                        fc[j * N + i] = cv;
+                    }
+                }
         }
     }
     __syncthreads();
@@ -1088,7 +1119,7 @@ int wc_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, 
         (K > 0 && (!empfc || !metrics)))
         return wc_set_err(WC_EINVAL, "wc_fc_metrics: bad arguments (7 <= N <= 96)");
     FcArgs a{B, N, M, K, bold, fc_in, empfc, phasor, fc_out, metrics, extra, data_range};
-    const size_t lds = (size_t)(2 * N * N + 8 + N) * sizeof(double);
+    const size_t lds = (size_t)(2 * ((N * N + 1) & ~1) + 8 + kMaxN + kFcThreads) * sizeof(double);
     hipError_t e = hipFuncSetAttribute((const void*)fc_metrics_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
