@@ -71,9 +71,10 @@ __device__ __forceinline__ float u01f(uint32_t x) { return (float)(2u * (x >> 9)
 __device__ __forceinline__ double u01d(uint32_t x) { return (double)(2u * (x >> 9) + 1u) * 5.9604644775390625e-8; }
 
 // the same u as u01f in two VALU ops: (1 + m 2^-23) - (1 - 2^-24) = (2m + 1) 2^-24
-// exactly (Sterbenz; the result is an odd multiple of 2^-24 below 1: 24 bits)
+// exactly (Sterbenz; the result is an odd multiple of 2^-24 below 1: 24 bits).  The
+// bits of 1 + m 2^-23 are one funnel shift: ({0x7F, x} >> 9) = 0x3F800000 | (x >> 9)
 __device__ __forceinline__ float u01f_fast(uint32_t x) {
-    return __uint_as_float((x >> 9) | 0x3F800000u) - 0.99999994039535522461f;
+    return __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, x, 9u)) - 0.99999994039535522461f;
 }
 
 // fp32, unscaled: z / sqrt(2 ln 2) = sqrt(-log2 u0) (cos, sin)(2 pi u1) -- the caller
@@ -167,6 +168,9 @@ __device__ __forceinline__ void split3(const float v[4], bf16x4& hi, bf16x4& mid
 // fp16 two-part split of v * 2^10 (v in [0, 1]): hi = fp16(RNE), lo = fp16(v 2^10 - hi);
 // v 2^10 - hi is exact in fp32, so hi + lo carries 22 significant bits and, scaled,
 // both parts stay normal fp16 down to v ~ 1e-4
+// lo = fp16(x - hi) in one v_fma_mix{lo,hi}_f16 per value: x (fp32) * 1 - hi (read as
+// fp16), rounded once to fp16; x - hi is exact in fp32, so the result is the same as
+// converting hi back, subtracting and converting (two ops fewer per pair)
 __device__ __forceinline__ void split2h(const float v[4], f16x4& hi, f16x4& lo) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
@@ -174,7 +178,10 @@ __device__ __forceinline__ void split2h(const float v[4], f16x4& hi, f16x4& lo) 
     for (int p = 0; p < 2; ++p) {
         const f2 x = (f2){v[2 * p], v[2 * p + 1]} * 1024.0f;
         const h2 h = __builtin_convertvector(x, h2);
-        const h2 l = __builtin_convertvector(x - __builtin_convertvector(h, f2), h2);
+        uint32_t lb;
+        asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lb) : "v"(x[0]), "v"(h));
+        asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lb) : "v"(x[1]), "v"(h));
+        const h2 l = __builtin_bit_cast(h2, lb);
         hi[2 * p] = h[0];
         hi[2 * p + 1] = h[1];
         lo[2 * p] = l[0];
