@@ -34,11 +34,20 @@ from nremmodfc_amd.model import Batch, driver_params, sim_keys  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 vector = FP32 matrix (MI355X_MICROARCH.md)
 PEAK_FP64_TFLOPS = 78.6
+PEAK_F16_TFLOPS = 2500.0   # dense fp16 MFMA (MI355X_MICROARCH.md); the fp16x3 coupling runs on it
 
 
 def flops_per_node_step(N):
     """2N coupling flops + 35 elementwise ops per node-step."""
     return 2 * N + 35
+
+
+def issued_mfma_flops_per_node_step(N):
+    """MFMA flops the f32 kernels actually issue per node-step: the coupling runs as three fp16
+    products (fp16x3) over nodes padded to 16 (N <= 96) or 64 (N > 96) on both sides."""
+    pad = 16 if N <= 96 else 64
+    Np = -(-N // pad) * pad
+    return 3 * 2 * Np * Np / N
 
 
 def sweep_batch(rank, n_seeds=50, nG=20, nS=20):
@@ -233,7 +242,14 @@ def main():
                                 "step_kernel (wc_sde_large.hip; %d launches of 1 Euler step, %d sims)" % (EULER, B)),
                      "kernel_ms_per_launch": kern["sde"],
                      "flops_per_node_step": fl,
-                     "pmc": util or None},
+                     "pmc": util or None,
+                     "issued_mfma": ({"dtype": "f16", "flops_per_node_step": issued_mfma_flops_per_node_step(N),
+                                      "tflops": per_launch_ns * issued_mfma_flops_per_node_step(N)
+                                      / (kern["sde"] * 1e-3) / 1e12,
+                                      "peak": PEAK_F16_TFLOPS,
+                                      "frac": per_launch_ns * issued_mfma_flops_per_node_step(N)
+                                      / (kern["sde"] * 1e-3) / 1e12 / PEAK_F16_TFLOPS}
+                                     if args.precision == "f32" else None)},
         "kernel_ms": kern,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
