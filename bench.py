@@ -201,7 +201,7 @@ def main():
     achieved = per_launch_ns * fl / (kern["sde"] * 1e-3) / 1e12
     traffic = None
     util = {}
-    pmc = os.path.join(ROOT, "profiles", "pmc_sde.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_sde.json" if args.config == "c3" else "pmc_sde_c5.json")
     if os.path.exists(pmc):
         try:
             d = json.load(open(pmc))

@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""Short C5 integrator run for rocprofv3 --pmc passes (tools/profile_c5.sh): the bench's C5 shard
+(2,500 simulations of the (G, sigma) grid on the 1000-node synthetic connectome), STEPS Euler steps
+recording every 20th into a node-major ring like bench.py --config c5 --sde-only."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from nremmodfc_amd import datasets  # noqa: E402
+from nremmodfc_amd.model import Batch, driver_params  # noqa: E402
+
+
+def main():
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 400
+    sc = datasets.synthetic_sc(1000)
+    G, S, keys = bench.sweep_batch(0)
+    G, S, keys = G[:2500], S[:2500], keys[:2500]
+    bt = Batch(sc, G, S, keys, driver_params(), precision="f32")
+    ring = torch.empty(2500 * 1000 * (steps // 20), dtype=bt.rec_dtype, device="cuda")
+    bt.integrate(steps, 2.0, 20, ring, rec_ld=steps // 20)
+    torch.cuda.synchronize()
+    print("ok", steps)
+
+
+if __name__ == "__main__":
+    main()
