@@ -79,3 +79,51 @@ def test_wc_run_checks_globals(cuda):
         wc.N = n
     with pytest.raises(NotImplementedError):
         wc.wilsonCowan()
+
+
+def test_cortex_run_flow(cuda, sc90):
+    """cortex_run.py:69-135 style: per-node G / sigmaE maps assigned to the module
+    globals, wilsonCowan.recompile(), run(), simBOLD at BOLD_downsamp=10, Kuramoto of
+    both the BOLD and the raw E_t, and the metrics against an empirical FC."""
+    from nremmodfc_amd import netwWilsonCowanPlastic as wc
+    from nremmodfc_amd import utils
+    from nremmodfc_amd.model import sim_keys
+    ach = datasets.load_map("DIST_VAChT_feobv_hc18_aghourian")
+    na = datasets.load_map("DIST_LC_proj")
+    G, S = 0.16 + 0.1 * ach, 7.68 - 0.12 * na
+    old = {k: getattr(wc, k) for k in ("CM", "G", "sigmaE", "rhoE", "P", "tTrans1", "tTrans2", "tstop", "timeTrans1",
+                                       "timeTrans2", "timeSim", "time", "sid", "precision")}
+    try:
+        wc.sigmaE, wc.G, wc.CM, wc.rhoE, wc.P = S, G, sc90, 0.14, 0.4
+        wc.precision = "f64"
+        wc.tTrans1, wc.tTrans2, tstop = 0.01, 0.1, 10.0
+        wc.timeTrans1 = np.arange(0, wc.tTrans1, wc.dtSim)
+        wc.timeTrans2 = np.arange(0, wc.tTrans2, wc.dtSim)
+        wc.tstop = tstop
+        wc.timeSim = np.arange(0, tstop, wc.dtSim)
+        wc.time = np.arange(0, tstop, wc.dt)
+        wc.sid = 11
+        wc.wilsonCowan.recompile()
+        tray = wc.run()
+        assert tray.shape == (len(wc.time), 3, 90)
+
+        ob = oracle.OracleBatch(sc90, G, S, sim_keys([11], [0]), wc._params())
+        ob.integrate(len(wc.timeTrans1), 0.05)
+        ob.integrate(len(wc.timeTrans2), 1.0)
+        rec = ob.integrate(len(wc.timeSim), 2.0, wc.downsamp)[0]
+        np.testing.assert_allclose(tray[:, 0, :], rec, rtol=0, atol=1e-9)
+
+        E_t = tray[:, 0, :]
+        bold = wc.simBOLD(E_t, nnodes=90, BOLD_downsamp=10)
+        want = osg.sim_bold(E_t, bold_downsamp=10)
+        assert bold.shape == want.shape == ((len(wc.time) - 2000 + 9) // 10, 90)
+        assert np.abs(bold - want).max() <= 1e-7 * np.abs(want).max()
+
+        np.testing.assert_allclose(utils.kuramoto(bold), osg.kuramoto(bold), rtol=1e-9)
+        np.testing.assert_allclose(utils.kuramoto(E_t), osg.kuramoto(E_t), rtol=1e-9)
+        sfc = np.corrcoef(bold.T)
+        got = utils.get_all_metrics(sfc, datasets.load_empfc("W"), data_range=1)
+        assert np.isfinite(got).all() and -1 <= got[0] <= 1
+    finally:
+        for k, v in old.items():
+            setattr(wc, k, v)
