@@ -152,6 +152,9 @@ enum : int {
     V_REC2 = 128,     // node-major E records buffered 2 deep: one 8-B store per node per 2 records
     V_REC4 = 256,     // ... 4 deep: one 16-B store per node per 4 records (host checks eligibility)
     V_F16X3 = 512,    // fp32 coupling as three fp16 cross terms of two-part (22-bit) operands
+    V_ZFIRST = 1024,  // fp32 fast path: the step's normals drawn before the coupling MFMAs
+    V_ILV = 2048,     // ... interleaved with them (sched_group_barrier: 1 MFMA, 6 VALU)
+    V_ILV2 = 4096,    // ... interleaved with them (1 MFMA, 2 VALU: the free half of a 16x16x32 gap)
 };
 
 // SG > 1: one workgroup holds SG groups of 16 simulations (SG x NW waves) that
@@ -176,6 +179,9 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr bool kParamRegs = sizeof(Real) == 4;  // fp64 re-reads G/sigmaE (register budget)
     // fp32 with the compensated a_ie: the folded-constant update (Sl holds -sigmaE log2 e)
     constexpr bool kFast = sizeof(Real) == 4 && kPairA;
+    constexpr bool kZFirst = kFast && kRng && (VAR & V_ZFIRST) != 0;
+    // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
+    constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
     constexpr int kFragUnits = kBf ? NT * NC * PS : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -383,6 +389,13 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         for (int u = 0; u < OT; ++u) acc[u] = acc_t{0, 0, 0, 0};
         int fl = lane;
         if constexpr (!kFragRegs || NW > 1) asm volatile("" : "+v"(fl));  // opaque: LDS reads stay in the loop
+        const uint64_t gstep = (uint64_t)(a.step0 + s);
+        // V_ZFIRST: the normals do not depend on the coupling, so they can fill the MFMA chain's gaps
+        float zz[kZFirst ? OT : 1][4];
+        if constexpr (kZFirst) {
+#pragma unroll
+            for (int u = 0; u < OT; ++u) quad_normals_raw(gstep, (uint32_t)(4 * (T0 + u) + g), key, zz[u]);
+        }
         if constexpr (kMfma && kBf) {
             const bf16x8* l16 = reinterpret_cast<const bf16x8*>(smem);
             const bf16x8* xb = xb16 + buf * NC * PS * 64;
@@ -445,14 +458,28 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             }
         }
 
+        if constexpr (kIlv > 0) {
+            // LDS reads first, then each MFMA followed by a slice of the (independent) normal generation
+#pragma unroll
+            for (int i = 0; i < NC * NP * (OT + 1); ++i) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+            for (int i = 0; i < NC * OT * kTerms; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, kIlv, 0);
+            }
+        }
         // ---- elementwise update (wc:77-83), noise drawn inside the E sigmoid ----
-        const uint64_t gstep = (uint64_t)(a.step0 + s);
 #pragma unroll
         for (int u = 0; u < OT; ++u) {
             if constexpr (sizeof(Real) == 8) __builtin_amdgcn_sched_barrier(0);  // fp64: bound live ranges
             Real z[4] = {0, 0, 0, 0};
             if constexpr (kFast) {
-                if constexpr (kRng) quad_normals_raw(gstep, (uint32_t)(4 * (T0 + u) + g), key, z);
+                if constexpr (kZFirst) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) z[r] = zz[u][r];
+                } else if constexpr (kRng) {
+                    quad_normals_raw(gstep, (uint32_t)(4 * (T0 + u) + g), key, z);
+                }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     // wc:80-83 in fp32 with the constants folded:
@@ -699,6 +726,10 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         // fp16 x3 coupling: grouped (as 15), register-resident (as 3)
         case 26: return launch_v<float, 6, 3, V_F16X3 | K, 1, 5>(ka, sc, ws, st);
         case 27: return launch_v<float, 6, 3, V_F16X3 | V_FRAG_REGS | K>(ka, sc, ws, st);
+        // the grouped fp16 product (26) with the normals drawn before / interleaved with the MFMAs
+        case 28: return launch_v<float, 6, 3, V_F16X3 | K | V_ZFIRST, 1, 5>(ka, sc, ws, st);
+        case 29: return launch_v<float, 6, 3, V_F16X3 | K | V_ZFIRST | V_ILV, 1, 5>(ka, sc, ws, st);
+        case 30: return launch_v<float, 6, 3, V_F16X3 | K | V_ZFIRST | V_ILV2, 1, 5>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
