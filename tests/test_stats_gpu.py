@@ -3,11 +3,12 @@
 The reference's runs are not seed-reproducible (numba RNG seeded from
 os.urandom), so the shipped tables pin the pipeline only statistically: for a
 grid cell, the mean over seeds of each of the 16 metric columns. This test runs
-four cells of the homogeneous sweep (whole_sweep_both.py) at the FULL 1001 s
+four cells of each shipped sweep -- homogeneous (whole_sweep_both.py), real maps
+and shuffled maps (whole_sweep_both_maps.py 1 1 / 2 2) -- at the FULL 1001 s
 schedule through the product pipeline (fp32 integrator, streamed BOLD /
 band-pass, FC + metrics, Welch peak), 30 seeds each, and compares every cell
 mean with the shipped one (tests/golden/shipped_cell_stats.npz, made by
-tests/golden/make_golden.py from output/sweep_delta_homo*.txt) as a z-score with
+tests/golden/make_golden.py from the three output/sweep_delta*.txt) as a z-score with
 the two-sample standard error sqrt(s1^2/n1 + s2^2/n2) -- tools/validate_stats.py
 restricted to four cells.
 
@@ -30,25 +31,28 @@ CELLS = [(5, 10), (0, 0), (19, 19), (10, 5)]
 SEEDS = 30
 
 
-def test_sweep_cells_match_shipped_statistics(cuda):
+@pytest.mark.parametrize("kind", ["homo", "maps", "shuf"])
+def test_sweep_cells_match_shipped_statistics(cuda, kind):
     st = np.load(GOLD)
     cols = list(st["columns"])
     assert cols == sweep.METRIC_COLS
     dGs, dSs = sweep._grids("shipped")
     want = {(round(float(dGs[i]), 4), round(float(dSs[j]), 4)) for i, j in CELLS}
-    sims = [s for s in sweep.homogeneous(n_iterations=SEEDS) if (round(s.dG, 4), round(s.dsigma, 4)) in want]
+    mid = {"homo": 0, "maps": 1, "shuf": 2}[kind]  # whole_sweep_both.py / _maps.py ids 1 1 and 2 2
+    sims = [s for s in sweep.maps(mid, mid, n_iterations=SEEDS, n_init=0)
+            if (round(s.dG, 4), round(s.dsigma, 4)) in want]
     assert len(sims) == len(CELLS) * SEEDS
     empfcs = {s: datasets.load_empfc(s) for s in sweep.STATES}
     rows, _ = sweep.run_sims(sims, datasets.load_sc(), empfcs)
 
-    ref_cells = {tuple(c): k for k, c in enumerate(st["homo_cells"])}
+    ref_cells = {tuple(c): k for k, c in enumerate(st[f"{kind}_cells"])}
     z = []
     for cell in sorted(want):
         vals = np.array([[r[c] for c in cols] for s, r in zip(sims, rows)
                          if (round(s.dG, 4), round(s.dsigma, 4)) == cell])
         assert vals.shape == (SEEDS, len(cols)) and np.isfinite(vals).all()
         k = ref_cells[cell]
-        rm, rs, rn = st["homo_mean"][k], st["homo_std"][k], st["homo_count"][k]
+        rm, rs, rn = st[f"{kind}_mean"][k], st[f"{kind}_std"][k], st[f"{kind}_count"][k]
         se = np.sqrt(vals.std(axis=0, ddof=1) ** 2 / SEEDS + rs ** 2 / rn)
         d = vals.mean(axis=0) - rm
         # a column constant over seeds on both sides (peakfreq is a spectral bin) must match exactly
