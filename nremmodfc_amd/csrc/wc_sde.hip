@@ -597,7 +597,7 @@ int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     if constexpr (hf) {
         const int total = NT * (NT / 2) * 64;
         float* scl = static_cast<float*>(ws) + hf_scale_offset(NT);
-        hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(256), 0, st, sc, ka.N, scl);
+        hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(1024), 0, st, sc, ka.N, scl);
         hipLaunchKernelGGL((build_frag_f16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
                            static_cast<const float*>(scl), static_cast<f16x8*>(ws));
         lds = (frag_regs ? 0 : (size_t)NT * (NT / 2) * 2 * 64 * 16) +

@@ -248,9 +248,23 @@ __device__ __forceinline__ void tile_of(const Geo& g, int& sb, int& mb) {
     mb = wid % MB;
 }
 
+// state arrays read and written once per step: DIAG 4 streams them past L2 (nontemporal), so that
+// the connectome image the next workgroups read stays resident
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_state(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st_state(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // one Euler step of every simulation; rec_row >= 0: record the state before the update
 // DIAG (ablation, tools/diag_large.py): 1 = no chunk fetch (LDS reused),
-// 2 = no MFMA, 3 = no epilogue state traffic (noise + math only), 0 = product
+// 2 = no MFMA, 3 = no epilogue state traffic (noise + math only), 4 = nontemporal state
+// loads/stores, 0 = product
 template <typename Real, int DIAG = 0, int STAGES = 2, bool PF = false>
 __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec_row, int buf) {
     typedef typename Tr<Real>::acc_t acc_t;
@@ -400,6 +414,7 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             real4* Iw = reinterpret_cast<real4*>(a.ws + g.o_I);
             real4* Ahw = reinterpret_cast<real4*>(a.ws + g.o_Ahi);
             constexpr bool kState = DIAG != 3;
+            constexpr bool kNT = DIAG == 4 && sizeof(Real) == 4;
             real4 Gv, Sv;
             if (sizeof(Real) == 4 && uni) {  // one (G, slope) per simulation (uniform_params_kernel)
                 const float2 gs = kState ? reinterpret_cast<const float2*>(a.ws + g.o_GS1)[live ? b : g.B - 1]
@@ -412,20 +427,22 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             }
             real4 Ev, Iv;
             if constexpr (kPF) Iv = pfI[v][u];
-            else Iv = kState ? Iw[t4] : real4{0.1, 0.1, 0.1, 0.1};
+            else Iv = kState ? ld_state<kNT>(Iw + t4) : real4{0.1, 0.1, 0.1, 0.1};
             AccA<sizeof(Real) == 4> Av[4];
             real4* Xn;  // next step's E image (f64) / tile-major E (f32)
             if constexpr (sizeof(Real) == 4) {
                 // E of this lane's 4 nodes (fp32 state, tile-major like I)
-                Ev = kState ? reinterpret_cast<const real4*>(a.ws + g.o_E)[t4] : real4{0.1, 0.1, 0.1, 0.1};
+                Ev = kState ? ld_state<kNT>(reinterpret_cast<const real4*>(a.ws + g.o_E) + t4)
+                            : real4{0.1, 0.1, 0.1, 0.1};
                 Xn = nullptr;
                 real4 hi, lo;
                 if constexpr (kPF) {
                     hi = pfH[v][u];
                     lo = pfL[v][u];
                 } else {
-                    hi = kState ? Ahw[t4] : real4{2.5, 2.5, 2.5, 2.5};
-                    lo = kState ? reinterpret_cast<const real4*>(a.ws + g.o_Alo)[t4] : real4{0, 0, 0, 0};
+                    hi = kState ? ld_state<kNT>(Ahw + t4) : real4{2.5, 2.5, 2.5, 2.5};
+                    lo = kState ? ld_state<kNT>(reinterpret_cast<const real4*>(a.ws + g.o_Alo) + t4)
+                                : real4{0, 0, 0, 0};
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -475,7 +492,7 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
                     Av[r].add(dtA * (in * (e - rhoE)));
                 }
             }
-            if (kState) Iw[t4] = In;
+            if (kState) st_state<kNT>(Iw + t4, In);
             if constexpr (sizeof(Real) == 4) {
                 // next step's B operand: the fp16 split of the new E 2^10
                 float ev[4] = {En[0], En[1], En[2], En[3]};
@@ -485,15 +502,15 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
 #pragma unroll
                 for (int p = 0; p < kParts; ++p) Xo[xs_index(g, p, b, n0) >> 2] = ph[p];
                 if (!kState) continue;
-                reinterpret_cast<real4*>(a.ws + g.o_E)[t4] = En;
+                st_state<kNT>(reinterpret_cast<real4*>(a.ws + g.o_E) + t4, En);
                 real4 hi, lo;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     hi[r] = Av[r].hi;
                     lo[r] = Av[r].lo;
                 }
-                Ahw[t4] = hi;
-                reinterpret_cast<real4*>(a.ws + g.o_Alo)[t4] = lo;
+                st_state<kNT>(Ahw + t4, hi);
+                st_state<kNT>(reinterpret_cast<real4*>(a.ws + g.o_Alo) + t4, lo);
             } else {
                 Xn[(size_t)(4 * mt + gq) * g.Bp + b] = En;
                 real4 av;
@@ -521,7 +538,7 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
     if constexpr (sizeof(Real) == 4) {
         const int n = g.MT * g.NC * 64;
         float* scl = reinterpret_cast<float*>(a.ws + g.o_scl);
-        hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(256), 0, st, sc, N, scl);
+        hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(1024), 0, st, sc, N, scl);
         hipLaunchKernelGGL(frag_f16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc, g, scl,
                            reinterpret_cast<f16x8*>(a.ws + g.o_frag));
     } else {
@@ -586,6 +603,8 @@ int wc_large_diag(int variant, const wc_params* p, int B, int N, const double* s
                                                       0, 0, nullptr, nullptr, nullptr, workspace, st);
         case 106: return run_large<float, 0, 3, false>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip,
                                                        0, 0, nullptr, nullptr, nullptr, workspace, st);
+        case 107: return run_large<float, 4>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, 0, 0,
+                                             nullptr, nullptr, nullptr, workspace, st);
         default: return wc_set_err(WC_EINVAL, "unknown large-N diagnostic variant");
     }
 }

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Ablation of the N > 96 step kernel (wc_diag_integrate variants 100..103):
 100 product, 101 no chunk fetch, 102 no MFMA, 103 no epilogue state traffic,
-104 3 stages + epilogue state prefetched, 105 2 stages + prefetch, 106 3 stages.
+104 3 stages + epilogue state prefetched, 105 2 stages + prefetch, 106 3 stages,
+107 nontemporal epilogue state loads/stores.
 Times us/step at N (default 1000) and B (default 2500); interleaved rounds."""
 import ctypes
 import os
@@ -24,7 +25,7 @@ def main():
     rng = np.random.default_rng(0)
     bt = Batch(sc, 0.16 + rng.uniform(-0.1, 0.3, B), 7.68 + rng.uniform(-0.2, 0.2, B),
                sim_keys(np.arange(B), np.zeros(B, dtype=np.int64)), precision="f32")
-    variants = [100, 101, 102, 103, 104, 105, 106]
+    variants = [int(v) for v in os.environ.get("DIAG_VARIANTS", "100,101,102,103,104,105,106,107").split(",")]
     times = {v: [] for v in variants}
     for r in range(3):
         for v in variants:
