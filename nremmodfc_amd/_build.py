@@ -12,6 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libwcsde.so")
+# A/B timing of two builds in one session (tools/): load another in-tree build instead
+LIB_LOAD = os.environ.get("WCSDE_LIB_OVERRIDE", LIB)
 ARCH = os.environ.get("WCSDE_ARCH", "gfx950")
 
 

@@ -9,7 +9,7 @@ import os
 
 import torch  # noqa: F401  (loads the process' HIP runtime before libwcsde.so)
 
-from ._build import LIB as LIB_PATH
+from ._build import LIB_LOAD as LIB_PATH
 
 WC_F32, WC_F64 = 0, 1
 
