@@ -287,9 +287,12 @@ def main(argv=None):
         rows, _ = run_sims(todo, sc, empfcs, sched, args.precision, args.batch, device, progress=Progress(rank))
         wall = time.perf_counter() - t0
         n_steps = len(todo) * sc.shape[0] * sched.n_total
-        print(json.dumps({"rank": rank, "sims": len(todo), "wall_s": wall, "node_steps": n_steps,
-                          "node_steps_per_s": n_steps / wall if wall else None,
-                          "batches": getattr(run_sims, "last_timings", None)}), flush=True)
+        perf = json.dumps({"rank": rank, "sims": len(todo), "wall_s": wall, "node_steps": n_steps,
+                           "node_steps_per_s": n_steps / wall if wall else None,
+                           "batches": getattr(run_sims, "last_timings", None)})
+        print(perf, flush=True)
+        with open(os.path.join(args.out, "temp", f"{tag}_rank{rank}_perf.jsonl"), "a") as f:  # one line per run
+            f.write(perf + "\n")
         append_rows(path, rank, todo, rows)
         table = rows_table(rank, todo, rows)
         if dist:

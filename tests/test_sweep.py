@@ -2,6 +2,7 @@
 formats and the shipped output tables (tests/golden/shipped_*_head.csv are the
 first rows of /root/reference/output/*.txt, copied by make_golden.py)."""
 import itertools
+import json
 import os
 
 import numpy as np
@@ -144,6 +145,9 @@ def test_sweep_main_short(tmp_path, cuda):
     assert (df["corrW"].abs() <= 1).all() and (df["peakfreq"] > 0).all()
     sweep.main(["homo", "--seeds", "1", "--short", "--limit", "6", "--out", out, "--tag", "t"])
     assert len(pd.read_csv(os.path.join(out, "t.txt"))) == 6
+    with open(os.path.join(out, "temp", "t_rank0_perf.jsonl")) as f:  # one perf line per invocation
+        perf = [json.loads(line) for line in f]
+    assert [p["sims"] for p in perf] == [6, 0] and perf[0]["node_steps_per_s"] > 0
 
 
 @pytest.mark.gpu
