@@ -34,6 +34,7 @@ from nremmodfc_amd.model import Batch, driver_params, sim_keys  # noqa: E402
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 vector = FP32 matrix (MI355X_MICROARCH.md)
 PEAK_FP64_TFLOPS = 78.6
+PEAK_HBM_GBPS = 8000.0     # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAK_F16_TFLOPS = 2500.0   # dense fp16 MFMA (MI355X_MICROARCH.md); the fp16x3 coupling runs on it
 
 
@@ -250,6 +251,14 @@ def main():
                      "kernel_ms_per_launch": kern["sde"],
                      "flops_per_node_step": fl,
                      "pmc": util or None,
+                     # the north star's "HBM roofline" wording, priced as a state-streaming
+                     # integrator would run (fp32 E, I, a_ie read + written per node-step = 24 B); this
+                     # kernel keeps the state in registers, so the fraction can exceed 1
+                     "hbm_state_streaming_equiv": {"bytes_per_node_step": 24,
+                                                   "GBps": per_launch_ns * 24 / (kern["sde"] * 1e-3) / 1e9,
+                                                   "peak_GBps": PEAK_HBM_GBPS,
+                                                   "frac": per_launch_ns * 24 / (kern["sde"] * 1e-3) / 1e9
+                                                   / PEAK_HBM_GBPS},
                      "issued_mfma": ({"dtype": "f16", "flops_per_node_step": issued_mfma_flops_per_node_step(N),
                                       "tflops": per_launch_ns * issued_mfma_flops_per_node_step(N)
                                       / (kern["sde"] * 1e-3) / 1e12,
