@@ -212,6 +212,15 @@ int wc_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, 
                   int K, double data_range, const double* phasor, double* fc_out, double* metrics,
                   double* extra, void* stream);
 
+/* np.corrcoef(x[:, b, :].T) for every simulation b of a long time-major series
+ * x [M][B][N] (the SC optimiser's FC, optimize_SC_Hopf.py:67-69: 6000 samples),
+ * split over time blocks so a small batch still fills the GPU; fc [B][N][N],
+ * clipped to [-1, 1].  2 <= N <= 96, M >= 2.  Deterministic (fixed blocks, fixed
+ * combine order).  workspace: wc_corrcoef_workspace_size(B, N, M) bytes. */
+size_t wc_corrcoef_workspace_size(int B, int N, int M);
+int wc_corrcoef(int B, int N, int M, const double* x, double* fc, void* workspace, size_t ws_bytes,
+                void* stream);
+
 /* utils.kuramoto (utils.py:34-40) from unit phasors [M][B][N][2] (wc_hilbert_phase):
  * out [B][2] = (mean_t R(t), std_t R(t)), R(t) = |mean_n exp(i theta_n(t))|. */
 int wc_kuramoto(int B, int N, int M, const double* phasor, double* out, void* stream);

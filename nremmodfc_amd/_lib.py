@@ -62,6 +62,8 @@ _SIGNATURES = {
     "wc_hilbert_phase": (c_int, [c_i64, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "wc_fc_metrics": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wc_kuramoto": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "wc_corrcoef_workspace_size": (c_sz, [c_int, c_int, c_int]),
+    "wc_corrcoef": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "wc_hma": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "wc_hopf_workspace_size": (c_sz, [c_int, c_int]),
     "wc_hopf_integrate": (c_int, [ctypes.POINTER(WCHopfParamsC), c_int, c_int, c_vp, c_vp, c_vp, c_vp,

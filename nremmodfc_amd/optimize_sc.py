@@ -10,8 +10,8 @@ epsilon * (empirical - simulated); clip at 0, keep the strongest 30% of links an
 restore the total weight.
 
 Every simulation of an iteration runs in one device launch (wc_hopf_integrate),
-the band-pass in one more (wc_filtfilt) and the FCs in one more
-(wc_fc_metrics); the per-iteration SC update is O(N^2) host bookkeeping, as in
+the band-pass in one more (wc_filtfilt) and the FCs in three more
+(wc_corrcoef, split over time blocks); the per-iteration SC update is O(N^2) host bookkeeping, as in
 the reference.
 
     python -m nremmodfc_amd.optimize_sc [--iters 100] [--seeds 10] [--out DIR]
@@ -75,7 +75,7 @@ def simulated_fc(seeds, device="cuda"):
     rc = L.wc_filtfilt(len(a) - 1, dp(b), dp(a), dp(zi), T, B * N, _lib.ptr(x), _lib.ptr(y), _lib.stream_handle())
     _lib.check(rc, "wc_filtfilt")
     cut0, cut1 = int(60 / res), int((HM.tmax - 60) / res)
-    fc, _, _ = sigchain.fc_metrics(y[cut0:cut1], B, N, None, kuramoto=False, want_fc=True)
+    fc = sigchain.corrcoef(y[cut0:cut1], B, N)  # split over time blocks: 10 series fill the GPU
     return fc.mean(dim=0).cpu().numpy()
 
 

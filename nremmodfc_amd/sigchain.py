@@ -200,3 +200,16 @@ def sim_bold(E_t, bold_downsamp=1000, neq=NEQ, bold_dt=0.04):
     bs = BoldStream(C, T, neq, bold_downsamp, bold_dt, E_t.device)
     bs.feed(E_t.reshape(T, C).contiguous())
     return bs.finish()
+
+
+def corrcoef(x, B, N):
+    """np.corrcoef(x[:, b, :].T) for every b of a time-major [M][B][N] fp64 device series
+    (wc_corrcoef: split over time blocks, for long series and small batches) -> [B][N][N]."""
+    L = _lib.lib()
+    x = x.contiguous()
+    M = x.shape[0]
+    fc = torch.empty((B, N, N), dtype=torch.float64, device=x.device)
+    ws = torch.empty(L.wc_corrcoef_workspace_size(B, N, M) // 8 + 1, dtype=torch.float64, device=x.device)
+    _lib.check(L.wc_corrcoef(B, N, M, _lib.ptr(x), _lib.ptr(fc), _lib.ptr(ws), ws.numel() * 8,
+                             _lib.stream_handle()), "wc_corrcoef")
+    return fc

@@ -74,3 +74,15 @@ def test_hma_validates_without_device_work():
     assert L.wc_hma(4, 90, None, vp, vp, vp, vp, None, None, None) == -1
     assert L.wc_hma(4, 97, vp, vp, vp, vp, vp, None, None, None) == -2
     assert b"96" in L.wc_last_error()
+
+
+def test_corrcoef_validates_without_device_work():
+    from nremmodfc_amd import _lib
+    L = _lib.lib()
+    vp = ctypes.c_void_p(16)
+    assert L.wc_corrcoef_workspace_size(10, 90, 6000) > 10 * 90 * 90 * 8
+    assert L.wc_corrcoef_workspace_size(0, 90, 6000) == 0
+    assert L.wc_corrcoef(10, 97, 6000, vp, vp, vp, 1 << 30, None) == -1  # N > 96
+    assert L.wc_corrcoef(10, 90, 1, vp, vp, vp, 1 << 30, None) == -1     # M < 2
+    assert L.wc_corrcoef(10, 90, 6000, vp, vp, vp, 64, None) == -3       # workspace
+    assert b"workspace" in L.wc_last_error()

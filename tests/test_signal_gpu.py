@@ -230,6 +230,16 @@ def test_pipeline_fc_ssim_vs_oracle(cuda, sc90):
         assert osg.ssim(res.fc[b], wfc, data_range=2.0) >= 0.999999
 
 
+@pytest.mark.parametrize("M,B,N", [(6000, 10, 90), (777, 3, 90), (65, 1, 7), (3, 2, 2), (6000, 300, 96)])
+def test_corrcoef_split_vs_numpy(cuda, M, B, N):
+    """wc_corrcoef (time-block split) vs np.corrcoef, incl. one block, tiny M and a batch past the split."""
+    rng = np.random.default_rng(M + B + N)
+    x = rng.standard_normal((M, B, N)).cumsum(0) * 0.01 + rng.standard_normal((1, B, N))
+    fc = wsg.corrcoef(torch.from_numpy(x).cuda(), B, N).cpu().numpy()
+    for b in range(B):
+        np.testing.assert_allclose(fc[b], np.corrcoef(x[:, b, :].T), rtol=0, atol=1e-12)
+
+
 @pytest.mark.parametrize("M", [6000, 777])
 def test_fc_long_series_vs_numpy(cuda, M):
     """wc_fc_metrics' corrcoef over long series (the SC optimiser's 6000-sample window)."""
