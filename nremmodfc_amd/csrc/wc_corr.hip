@@ -4,11 +4,12 @@
 // np.corrcoef(x[cut0:cut1].T) per seed, 6000 samples x 90 nodes, 10 seeds). One
 // workgroup per simulation (wc_fc_metrics) keeps 10 CUs busy; here every
 // simulation's series is cut into time blocks so that B x nblk workgroups share the
-// work, in three stream-ordered launches:
+// work, in four stream-ordered launches:
 //   1. block sums of every node            -> part[b][k][n]
 //   2. means (block sums in block order), centred cross products of the block as
 //      4 x 4 register tiles of the upper triangle -> covp[b][k][i][j] (i <= j)
-//   3. sum over blocks in block order, 1/(M-1), corrcoef scaling and [-1, 1] clip.
+//   3. sum over blocks in block order, 1/(M-1), corrcoef scaling and [-1, 1] clip
+//      (standard deviations first, then one workgroup per row).
 // Two-pass (np.cov centres before multiplying), deterministic: fixed block sizes
 // and a fixed combine order, independent of the launch's scheduling.
 #include <hip/hip_runtime.h>
@@ -128,28 +129,40 @@ __global__ void __launch_bounds__(kThreads) block_cov_kernel(int B, int N, int M
     }
 }
 
-// 3. fc[b] = corrcoef from the summed blocks (np.corrcoef: c / sd_i / sd_j, clipped)
-__global__ void __launch_bounds__(kThreads) corr_finish_kernel(int N, int M, int nblk, const double* __restrict__ covp,
-                                                               double* __restrict__ fc) {
-    __shared__ double sd[kMaxN];
-    const int b = blockIdx.x;
-    const int NN = N * N;
-    const double* cb = covp + (int64_t)b * nblk * NN;
+// 3a. sd[b][n] = sqrt(cov_nn) from the summed blocks
+__global__ void __launch_bounds__(kThreads) corr_sd_kernel(int B, int N, int M, int nblk,
+                                                           const double* __restrict__ covp, double* __restrict__ sd) {
+    const int i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= B * N) return;
+    const int b = i / N, n = i % N;
+    const int64_t NN = (int64_t)N * N;
+    const double* cb = covp + (int64_t)b * nblk * NN + n * N + n;
+    double s = 0.0;
+    for (int q = 0; q < nblk; ++q) s += cb[q * NN];
+    sd[i] = sqrt(s * (1.0 / (M - 1)));
+}
+
+// 3b. row i of fc[b] (np.corrcoef: c / sd_i / sd_j, clipped), one workgroup per (b, i):
+// the blocks hold the upper triangle, summed in block order for j >= i and mirrored
+__global__ void __launch_bounds__(128) corr_row_kernel(int N, int M, int nblk, const double* __restrict__ covp,
+                                                       const double* __restrict__ sd, double* __restrict__ fc) {
+    const int b = blockIdx.x / N, i = blockIdx.x % N;
+    const int64_t NN = (int64_t)N * N;
+    const double* cb = covp + (int64_t)b * nblk * NN + (int64_t)i * N;
+    const double* sdb = sd + (int64_t)b * N;
     const double fact = 1.0 / (M - 1);
-    for (int n = threadIdx.x; n < N; n += kThreads) {
+    for (int j = i + threadIdx.x; j < N; j += 128) {
         double s = 0.0;
-        for (int q = 0; q < nblk; ++q) s += cb[(int64_t)q * NN + n * N + n];
-        sd[n] = sqrt(s * fact);
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < NN; e += kThreads) {
-        const int i = e / N, j = e % N;
-        const int lo = i < j ? i : j, hi = i < j ? j : i;  // blocks hold the upper triangle
-        double s = 0.0;
-        for (int q = 0; q < nblk; ++q) s += cb[(int64_t)q * NN + lo * N + hi];
-        double v = (s * fact) / sd[i];
-        v = v / sd[j];
-        fc[(int64_t)b * NN + e] = fmin(1.0, fmax(-1.0, v));
+        for (int q = 0; q < nblk; ++q) s += cb[q * NN + j];
+        double v = (s * fact) / sdb[i];
+        v = v / sdb[j];
+        v = fmin(1.0, fmax(-1.0, v));
+        fc[(int64_t)b * NN + (int64_t)i * N + j] = v;
+        if (j != i) {  // np.corrcoef: c[j][i] / sd_j / sd_i (division order as numpy, not mirrored bits)
+            double w = (s * fact) / sdb[j];
+            w = w / sdb[i];
+            fc[(int64_t)b * NN + (int64_t)j * N + i] = fmin(1.0, fmax(-1.0, w));
+        }
     }
 }
 
@@ -160,7 +173,7 @@ extern "C" {
 size_t wc_corrcoef_workspace_size(int B, int N, int M) {
     if (B <= 0 || N <= 0 || M <= 0) return 0;
     const CorrGeo g = corr_geo(B, M);
-    return (part_doubles(B, N, g) + (size_t)B * g.nblk * N * N) * sizeof(double);
+    return (part_doubles(B, N, g) + (size_t)B * g.nblk * N * N + (size_t)B * N) * sizeof(double);
 }
 
 int wc_corrcoef(int B, int N, int M, const double* x, double* fc, void* workspace, size_t ws_bytes, void* stream) {
@@ -177,7 +190,10 @@ int wc_corrcoef(int B, int N, int M, const double* x, double* fc, void* workspac
     const dim3 grid((unsigned)(B * g.nblk));
     hipLaunchKernelGGL(block_sum_kernel, grid, dim3(kThreads), 0, st, B, N, M, g.tb, g.nblk, x, part);
     hipLaunchKernelGGL(block_cov_kernel, grid, dim3(kThreads), 0, st, B, N, M, g.tb, g.nblk, x, part, covp);
-    hipLaunchKernelGGL(corr_finish_kernel, dim3(B), dim3(kThreads), 0, st, N, M, g.nblk, covp, fc);
+    double* sd = covp + (size_t)B * g.nblk * N * N;
+    hipLaunchKernelGGL(corr_sd_kernel, dim3((unsigned)((B * N + kThreads - 1) / kThreads)), dim3(kThreads), 0, st, B,
+                       N, M, g.nblk, covp, sd);
+    hipLaunchKernelGGL(corr_row_kernel, dim3((unsigned)(B * N)), dim3(128), 0, st, N, M, g.nblk, covp, sd, fc);
     return wc_hip_check("wc_corrcoef");
 }
 
