@@ -21,6 +21,7 @@ final C: the reference's commented-out np.savetxt, optimize_SC_Hopf.py:106).
 """
 import argparse
 import ctypes
+import functools
 import json
 import os
 import time
@@ -52,6 +53,7 @@ def configure(sc):
     HM.seed = 0
 
 
+@functools.lru_cache(maxsize=8)
 def band(resolution, fmin=0.01, fmax=0.1):
     """signal.bessel(3, [2 res Fmin, 2 res Fmax], 'bandpass') (optimize_SC_Hopf.py:62-64) and
     lfilter_zi: SciPy's own design routines (seven coefficients, host); the
