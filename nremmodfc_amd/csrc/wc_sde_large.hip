@@ -378,8 +378,7 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
     } else {
         const double* F = reinterpret_cast<const double*>(a.ws + g.o_frag);
         const double* X = reinterpret_cast<const double*>(a.ws + (buf ? g.o_X1 : g.o_X0));
-#pragma unroll 4
-        for (int c = 0; c < g.KC4; ++c) {
+        for (int c = 0; c < g.KC4; ++c) {  // (fp64 parity path: a requested unroll here does not apply)
             double fa[NU], fb[NV];
 #pragma unroll
             for (int u = 0; u < NU; ++u) fa[u] = F[((size_t)(m0 + u) * g.KC4 + c) * 64 + lane];
