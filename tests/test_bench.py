@@ -1,0 +1,47 @@
+"""bench.py keeps the driver's JSON contract (task spec).
+
+CPU: the cpu_baseline leg (the oracle's C loop, kind "port") on a short sample.
+GPU: one short bench run as a child process; its single JSON line carries every
+contract key, the roofline and issued-MFMA objects, and consistent arithmetic.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_cpu_baseline_leg():
+    sys.path.insert(0, ROOT)
+    import bench
+    from nremmodfc_amd import datasets
+    cb = bench.cpu_baseline(datasets.load_sc(), seconds=0.3, steps=200)
+    assert cb["kind"] == "port" and cb["unit"] == "node-timesteps/sec"
+    assert cb["value"] > 0 and 1 <= cb["cores"] <= 16 and "oracle/wc_oracle.c" in cb["sample"]
+
+
+@pytest.mark.gpu
+def test_bench_json_contract(cuda):
+    out = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--cpu-seconds", "1"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["metric"].startswith("node-timesteps/sec") and d["unit"] == "node-timesteps/sec"
+    assert d["n_gpus"] == 1 and d["steps"] == 1 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["scaling"] == "weak" and d["vs_baseline"] is None and d["dtype"] == "f32"
+    assert "workload" in d["config"] and d["config"]["sims_per_gpu"] == 20000
+    # value = node-steps of the timed steps / wall time
+    ns = d["config"]["sims_per_gpu"] * d["config"]["nodes"] * d["config"]["euler_steps_per_step"] * d["steps"]
+    assert abs(ns / (d["ms_per_step"] * 1e-3 * d["steps"]) / d["value"] - 1) < 1e-6
+    r = d["roofline"]
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    assert 0 < r["frac"] < 1.2 and r["issued_mfma"]["dtype"] == "f16"
+    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["value"] > 0
