@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define WCSDE_ABI_VERSION 3
+#define WCSDE_ABI_VERSION 4
 
 /* Noise stream (the reference's numba RNG is seeded from os.urandom and never
  * reproducible; the build defines its own): Philox4x32-10 with
@@ -94,9 +94,11 @@ size_t wc_workspace_size(int B, int N, int precision);
  *  rec_ld    0: records time-major [n_rec][B][N] (Y_t[:, k, :] of run());
  *            > 0: node-major, record k of column c = b*N + n at c*rec_ld + k
  *            (a slot of the sweep pipeline's E ring, read by BOLD and Welch).
- *  precision WC_F32: E, I, sigmoids in fp32; coupling as six bf16 MFMA cross
- *            terms of 3-way split operands with fp32 accumulation (fp32-
- *            equivalent); a_ie as a compensated fp32 pair;
+ *  precision WC_F32: E, I, sigmoids in fp32; coupling CM.E on the fp16 MFMA:
+ *            CM*sA and E*2^10 each split into two fp16 parts (hi + lo, 22
+ *            significant bits), three cross terms (lo.hi, hi.lo, hi.hi) with
+ *            fp32 accumulation, 1/(2^10 sA) folded into G; a_ie as a
+ *            compensated fp32 pair;
  *            WC_F64: everything fp64 (the parity mode).
  *  N <= 96   one launch integrates all nsteps with the state in registers;
  *  N > 96    one GEMM-shaped launch per Euler step (wc_sde_large.hip), the
@@ -207,16 +209,22 @@ int wc_hilbert_phase(int64_t C, int M, const double* x, double* phasor, void* wo
  *   fc_out [B][N][N]  np.corrcoef(BOLD.T)                (may be NULL)
  *   metrics [B][K][4] utils.get_all_metrics(sFC, empfc[k], data_range) = corr, euc, ssim, new_metric
  *   extra [B][3]      np.mean(sFC), kuramoto sync, meta (sync/meta 0 if phasor NULL)
- * 7 <= N <= 96. */
+ * N >= 7 (the SSIM window).  N <= 96: one workgroup per simulation with the FC in
+ * LDS, no workspace (may be NULL).  N > 96 (config 5, N = 1000): the FC is tiled
+ * through global memory (wc_fc_large.hip) and workspace must hold
+ * wc_fc_metrics_workspace_size(B, N, M, K, fc_out != NULL) bytes (it includes
+ * the B N^2 doubles of FC when fc_out is NULL).  Deterministic for every N. */
+size_t wc_fc_metrics_workspace_size(int B, int N, int M, int K, int want_fc);
 int wc_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, const double* empfc,
                   int K, double data_range, const double* phasor, double* fc_out, double* metrics,
-                  double* extra, void* stream);
+                  double* extra, void* workspace, size_t ws_bytes, void* stream);
 
 /* np.corrcoef(x[:, b, :].T) for every simulation b of a long time-major series
  * x [M][B][N] (the SC optimiser's FC, optimize_SC_Hopf.py:67-69: 6000 samples),
  * split over time blocks so a small batch still fills the GPU; fc [B][N][N],
- * clipped to [-1, 1].  2 <= N <= 96, M >= 2.  Deterministic (fixed blocks, fixed
- * combine order).  workspace: wc_corrcoef_workspace_size(B, N, M) bytes. */
+ * clipped to [-1, 1].  N >= 2, M >= 2 (N > 96: 64 x 64 covariance tiles in
+ * global memory, wc_fc_large.hip).  Deterministic (fixed blocks, fixed combine
+ * order).  workspace: wc_corrcoef_workspace_size(B, N, M) bytes. */
 size_t wc_corrcoef_workspace_size(int B, int N, int M);
 int wc_corrcoef(int B, int N, int M, const double* x, double* fc, void* workspace, size_t ws_bytes,
                 void* stream);
@@ -241,16 +249,6 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
                         int64_t nslots, int64_t seg0, const void* workspace, double* acc, void* stream);
 int wc_welch_peak(int B, int N, int nseg, double fs, const double* acc, double* peak, double* psd,
                   void* stream);
-
-/* Diagnostic: wc_integrate (WC_F32, no recI/recA) through compile-time kernel
- * variant `variant` (ablations / alternative tilings, see wc_sde.hip
- * launch_diag); 81 <= N <= 96 only.  Not part of the product path. */
-int wc_diag_integrate(int variant, const wc_params* p, int B, int N,
-                      const double* sc, const double* G, const double* sigmaE,
-                      const uint64_t* keys, double* E, double* I, double* A,
-                      int64_t step0, int64_t nsteps, double tau_ip,
-                      int64_t rec_every, void* recE,
-                      void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -51,8 +51,6 @@ _SIGNATURES = {
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_i64, c_i64, c_dbl, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "wc_noise": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_vp]),
-    "wc_diag_integrate": (c_int, [c_int, ctypes.POINTER(WCParamsC), c_int, c_int, c_vp, c_vp, c_vp, c_vp,
-                                  c_vp, c_vp, c_vp, c_i64, c_i64, c_dbl, c_i64, c_vp, c_vp, c_sz, c_vp]),
     "wc_bold_blocks": (c_i64, [ctypes.POINTER(WCBoldCfgC)]),
     "wc_bold_state_doubles": (c_sz, [ctypes.POINTER(WCBoldCfgC), c_i64]),
     "wc_bold_init": (c_int, [ctypes.POINTER(WCBoldCfgC), c_i64, c_vp, c_vp]),
@@ -60,7 +58,9 @@ _SIGNATURES = {
                               c_vp]),
     "wc_bold_finish": (c_int, [ctypes.POINTER(WCBoldCfgC), c_i64, c_vp, c_vp, c_vp]),
     "wc_hilbert_phase": (c_int, [c_i64, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
-    "wc_fc_metrics": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wc_fc_metrics_workspace_size": (c_sz, [c_int, c_int, c_int, c_int, c_int]),
+    "wc_fc_metrics": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
+                              c_vp]),
     "wc_kuramoto": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "wc_corrcoef_workspace_size": (c_sz, [c_int, c_int, c_int]),
     "wc_corrcoef": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),

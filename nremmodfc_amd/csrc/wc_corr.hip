@@ -17,6 +17,11 @@
 #include <stdint.h>
 #include "wc_common.h"
 
+// N > 96: wc_fc_large.hip (FC tiles in global memory)
+size_t wc_large_corrcoef_workspace_size(int B, int N);
+int wc_large_corrcoef(int B, int N, int M, const double* x, double* fc, void* workspace, size_t ws_bytes,
+                      hipStream_t st);
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -172,14 +177,16 @@ extern "C" {
 
 size_t wc_corrcoef_workspace_size(int B, int N, int M) {
     if (B <= 0 || N <= 0 || M <= 0) return 0;
+    if (N > kMaxN) return wc_large_corrcoef_workspace_size(B, N);
     const CorrGeo g = corr_geo(B, M);
     return (part_doubles(B, N, g) + (size_t)B * g.nblk * N * N + (size_t)B * N) * sizeof(double);
 }
 
 int wc_corrcoef(int B, int N, int M, const double* x, double* fc, void* workspace, size_t ws_bytes, void* stream) {
     wc_clear_err();
-    if (B <= 0 || N < 2 || N > kMaxN || M < 2 || !x || !fc)
-        return wc_set_err(WC_EINVAL, "wc_corrcoef: needs B >= 1, 2 <= N <= 96, M >= 2 and non-NULL x, fc");
+    if (B <= 0 || N < 2 || M < 2 || !x || !fc)
+        return wc_set_err(WC_EINVAL, "wc_corrcoef: needs B >= 1, N >= 2, M >= 2 and non-NULL x, fc");
+    if (N > kMaxN) return wc_large_corrcoef(B, N, M, x, fc, workspace, ws_bytes, static_cast<hipStream_t>(stream));
     if (!workspace || ws_bytes < wc_corrcoef_workspace_size(B, N, M))
         return wc_set_err(WC_EWORKSPACE, "wc_corrcoef: workspace too small");
     const CorrGeo g = corr_geo(B, M);

@@ -38,9 +38,11 @@ int wc_large_integrate(const wc_params* p, int precision, int B, int N, const do
                        const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
                        int64_t nsteps, double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI,
                        void* recA, void* workspace, hipStream_t st);
+#ifdef WCSDE_DIAG
 int wc_large_diag(int variant, const wc_params* p, int B, int N, const double* sc, const double* G,
                   const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
                   int64_t nsteps, double tau_ip, void* workspace, hipStream_t st);
+#endif
 
 namespace {
 using namespace wcdev;
@@ -690,7 +692,9 @@ int launch_f64(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     }
 }
 
-// diagnostic variants (81 <= N <= 96, fp32) for on-GPU ablation
+#ifdef WCSDE_DIAG
+// diagnostic variants (81 <= N <= 96, fp32) for on-GPU ablation; compiled only into
+// libwcsde_diag.so (python -m nremmodfc_amd._build --diag), never into the product library
 int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     constexpr int K = V_KAHAN_A;
     switch (variant) {
@@ -730,9 +734,17 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 28: return launch_v<float, 6, 3, V_F16X3 | K | V_ZFIRST, 1, 5>(ka, sc, ws, st);
         case 29: return launch_v<float, 6, 3, V_F16X3 | K | V_ZFIRST | V_ILV, 1, 5>(ka, sc, ws, st);
         case 30: return launch_v<float, 6, 3, V_F16X3 | K | V_ZFIRST | V_ILV2, 1, 5>(ka, sc, ws, st);
+        // small batches (strong-scaling shards): more waves per group of 16 simulations
+        case 31: return launch_v<float, 6, 6, V_F16X3 | V_FRAG_REGS | K>(ka, sc, ws, st);
+        case 32: return launch_v<float, 6, 6, V_F16X3 | V_FRAG_REGS | K | V_ZFIRST>(ka, sc, ws, st);
+        case 33: return launch_v<float, 6, 3, V_F16X3 | V_FRAG_REGS | K | V_ZFIRST>(ka, sc, ws, st);
+        case 34: return launch_v<float, 6, 6, V_F16X3 | K>(ka, sc, ws, st);
+        case 35: return launch_v<float, 6, 6, V_F16X3 | V_FRAG_REGS | K | V_ZFIRST | V_ILV2>(ka, sc, ws, st);
+        case 36: return launch_v<float, 6, 2, V_F16X3 | V_FRAG_REGS | K | V_ZFIRST>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
+#endif  // WCSDE_DIAG
 
 int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
               const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
@@ -793,6 +805,8 @@ int wc_integrate(const wc_params* p, int precision, int B, int N, const double* 
     return precision == WC_F64 ? launch_f64(ka, sc, workspace, st) : launch_f32(ka, sc, workspace, st);
 }
 
+#ifdef WCSDE_DIAG
+// declared in csrc/wcsde_diag.h (tools only)
 int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const double* sc, const double* G,
                       const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
                       int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* workspace,
@@ -813,6 +827,7 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
     if (ws_bytes < wc_workspace_size(B, N, WC_F32)) return wc_set_err(WC_EWORKSPACE, "wc_diag_integrate: workspace");
     return launch_diag(variant, ka, sc, workspace, static_cast<hipStream_t>(stream));
 }
+#endif  // WCSDE_DIAG
 
 int wc_noise(int precision, int B, int N, const uint64_t* keys, int64_t step, void* out, void* stream) {
     wc_clear_err();

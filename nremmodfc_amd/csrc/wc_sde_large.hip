@@ -583,7 +583,8 @@ int wc_large_integrate(const wc_params* p, int precision, int B, int N, const do
                             recI, recA, workspace, st);
 }
 
-// ablation variants of the fp32 step kernel (wc_diag_integrate variants 100..103)
+#ifdef WCSDE_DIAG
+// ablation variants of the fp32 step kernel (wc_diag_integrate variants 100..107; diag build only)
 int wc_large_diag(int variant, const wc_params* p, int B, int N, const double* sc, const double* G,
                   const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
                   int64_t nsteps, double tau_ip, void* workspace, hipStream_t st) {
@@ -607,3 +608,4 @@ int wc_large_diag(int variant, const wc_params* p, int B, int N, const double* s
         default: return wc_set_err(WC_EINVAL, "unknown large-N diagnostic variant");
     }
 }
+#endif  // WCSDE_DIAG

@@ -31,6 +31,12 @@
 #include <cstdlib>
 #include "wc_common.h"
 
+// N > 96: wc_fc_large.hip
+size_t wc_large_fc_metrics_workspace_size(int B, int N, int K, int own_fc);
+int wc_large_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, const double* empfc, int K,
+                        double data_range, const double* kur, double* fc_out, double* metrics, double* extra,
+                        void* workspace, size_t ws_bytes, hipStream_t st);
+
 namespace {
 
 
@@ -1111,19 +1117,36 @@ int wc_kuramoto(int B, int N, int M, const double* phasor, double* out, void* st
     return wc_hip_check("wc_kuramoto");
 }
 
+size_t wc_fc_metrics_workspace_size(int B, int N, int M, int K, int want_fc) {
+    if (B <= 0 || N <= kMaxN || M < 2 || K < 0) return 0;  // N <= 96: everything in LDS
+    return wc_large_fc_metrics_workspace_size(B, N, K, !want_fc) + 2 * (size_t)B * sizeof(double);
+}
+
 int wc_fc_metrics(int B, int N, int M, const double* bold, const double* fc_in, const double* empfc, int K,
                   double data_range, const double* phasor, double* fc_out, double* metrics, double* extra,
-                  void* stream) {
+                  void* workspace, size_t ws_bytes, void* stream) {
     wc_clear_err();
-    if (B <= 0 || N < 7 || N > 96 || M < 2 || K < 0 || (!bold && !fc_in) || !extra ||
-        (K > 0 && (!empfc || !metrics)))
-        return wc_set_err(WC_EINVAL, "wc_fc_metrics: bad arguments (7 <= N <= 96)");
+    if (B <= 0 || N < 7 || M < 2 || K < 0 || (!bold && !fc_in) || !extra || (K > 0 && (!empfc || !metrics)))
+        return wc_set_err(WC_EINVAL, "wc_fc_metrics: bad arguments (N >= 7)");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (N > kMaxN) {
+        const size_t need = wc_fc_metrics_workspace_size(B, N, M, K, fc_out != nullptr);
+        if (!workspace || ws_bytes < need)
+            return wc_set_err(WC_EWORKSPACE, "wc_fc_metrics: workspace < wc_fc_metrics_workspace_size() for N > 96");
+        double* kur = nullptr;
+        if (phasor) {
+            kur = reinterpret_cast<double*>(static_cast<char*>(workspace) + need) - 2 * (size_t)B;
+            hipLaunchKernelGGL(kuramoto_kernel, dim3(B), dim3(256), 0, st, B, N, M, phasor, kur);
+        }
+        return wc_large_fc_metrics(B, N, M, bold, fc_in, empfc, K, data_range, kur, fc_out, metrics, extra, workspace,
+                                   need - 2 * (size_t)B * sizeof(double), st);
+    }
     FcArgs a{B, N, M, K, bold, fc_in, empfc, phasor, fc_out, metrics, extra, data_range};
     const size_t lds = (size_t)(2 * ((N * N + 1) & ~1) + 8 + kMaxN + kFcThreads) * sizeof(double);
     hipError_t e = hipFuncSetAttribute((const void*)fc_metrics_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
-    hipLaunchKernelGGL(fc_metrics_kernel, dim3(B), dim3(kFcThreads), lds, static_cast<hipStream_t>(stream), a);
+    hipLaunchKernelGGL(fc_metrics_kernel, dim3(B), dim3(kFcThreads), lds, st, a);
     return wc_hip_check("wc_fc_metrics");
 }
 

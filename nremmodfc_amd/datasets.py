@@ -36,7 +36,12 @@ def load_empfc(state):
 def load_map(name, n=90):
     """Map normalised to mean 1 (whole_sweep_both_maps.py:47-57); HOMO = ones.
     The division happens in the file's dtype (float32 for the VAChT maps), as
-    the reference does, and only then is widened to float64."""
+    the reference does, and only then is widened to float64.  For n != 90 (the
+    synthetic connectome) the maps are synthetic_map()s: ACh seed 1001, NA seed
+    1002, the SHUFFLED_* names a fixed permutation of them."""
+    if name != "HOMO" and n != 90:
+        m = synthetic_map(n, 1001 if "VAChT" in name else 1002)
+        return m[np.random.default_rng(7).permutation(n)] if name.startswith("SHUFFLED") else m
     m = np.ones(n) if name == "HOMO" else np.load(os.path.join(DATA, name + ".npy"))
     return (m / m.mean()).astype(np.float64)
 

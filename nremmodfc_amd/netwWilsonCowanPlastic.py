@@ -56,7 +56,7 @@ sid = 12
 
 # ---- network (wc:61-68): the reference draws a random CM after np.random.seed(12) ----
 G = 0.7
-CM = np.random.default_rng(12).uniform(size=(90, 90))
+CM = np.random.RandomState(12).uniform(size=(90, 90))  # = np.random.seed(12); np.random.uniform(size=(90, 90))
 nnodes = len(CM)
 N = len(CM)
 

@@ -59,6 +59,18 @@ class SweepResult:
         return out
 
 
+def check_supported(N, schedule: Schedule = None, chunk_samples: int = 1000):
+    """Raise before any device work if the pipeline cannot produce every output for
+    an N-node connectome on this schedule (the epilogue's limits included)."""
+    sch = schedule or Schedule()
+    if N < 7:
+        raise ValueError("the SSIM of get_all_metrics needs N >= 7 (7x7 window, utils.py:48)")
+    if WELCH_HOP % chunk_samples or (sch.n_sim % sch.rec_every):
+        raise ValueError("chunk_samples must divide 2000 and n_sim must be a multiple of rec_every")
+    if sch.n_sim // sch.rec_every < NEQ + 16:
+        raise ValueError(f"simBOLD needs at least {NEQ + 16} recorded samples (Neq + filtfilt padlen)")
+
+
 def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedule: Schedule = None,
               params: WCParams = None, precision: str = F32, chunk_samples: int = 1000,
               bold_downsamp: int = 1000, max_launch_steps: int = 500_000, want_fc=False, want_bold=False,
@@ -67,8 +79,7 @@ def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedul
     sch = schedule or Schedule()
     p = params or driver_params()
     R = sch.rec_every
-    if WELCH_HOP % chunk_samples or (sch.n_sim % R):
-        raise ValueError("chunk_samples must divide 2000 and n_sim must be a multiple of rec_every")
+    check_supported(np.asarray(sc).shape[0], sch, chunk_samples)
     T = sch.n_sim // R  # recorded samples = len(wc.time)
     t_start = time.perf_counter()
     bt = Batch(sc, G, sigmaE, keys, p, precision, device)
@@ -109,6 +120,7 @@ def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedul
             next_seg += 1
         if progress:
             progress("recorded", bt.step, sch.n_total)
+    torch.cuda.synchronize(bt.device)  # the phase timings below are of finished work, not queued launches
     t_sde = time.perf_counter()
     # ---- epilogue ----
     states = tuple(empfcs.keys()) if empfcs else ()

@@ -109,8 +109,11 @@ def fc_metrics(bold=None, B=None, N=None, empfc=None, fc_in=None, kuramoto=True,
     extra = torch.empty((B, 3), dtype=torch.float64, device=dev)
     fc = torch.empty((B, N, N), dtype=torch.float64, device=dev) if want_fc else None
     ph = hilbert_phase(bold) if kuramoto else None
+    nws = L.wc_fc_metrics_workspace_size(B, N, M, K, int(want_fc))  # 0 for N <= 96
+    ws = torch.empty(nws // 8 + 1, dtype=torch.float64, device=dev) if nws else None
     rc = L.wc_fc_metrics(B, N, M, _lib.ptr(bold) if bold is not None else None, _lib.ptr(fc_in), _lib.ptr(emp), K,
-                         float(data_range), _lib.ptr(ph), _lib.ptr(fc), _lib.ptr(metrics), _lib.ptr(extra), _lib.stream_handle())
+                         float(data_range), _lib.ptr(ph), _lib.ptr(fc), _lib.ptr(metrics), _lib.ptr(extra),
+                         _lib.ptr(ws), nws, _lib.stream_handle())
     _lib.check(rc, "wc_fc_metrics")
     return fc, metrics[:, :K], extra
 

@@ -142,12 +142,19 @@ def collapse(paths, out_csv):
 
 
 def run_sims(sims: List[Sim], sc, empfcs, schedule=None, precision="f32", batch=20_000, device="cuda",
-             want_fc=False, progress=None):
-    """Run simulations through the GPU pipeline in batches -> (list of metric dicts, FCs or None)."""
+             want_fc=False, progress=None, on_batch=None):
+    """Run simulations through the GPU pipeline in batches -> (list of metric dicts, FCs or None).
+
+    on_batch(part, rows) is called after every batch (the drivers append and flush
+    the batch's rows there, so a crash loses at most the running batch).  Without
+    empirical FCs (e.g. the 1000-node synthetic connectome) the goodness-of-fit
+    columns are NaN."""
     from .model import sim_keys
     from .pipeline import run_sweep
     rows, fcs = [], []
     timings = []
+    if sims:  # at most ~2.5 M node-columns per batch (N = 1000: 2,500 sims, ~80 GB of ring + BOLD state)
+        batch = max(1, min(batch, 2_500_000 // len(sims[0].G)))
     for b0 in range(0, len(sims), batch):
         part = sims[b0:b0 + batch]
         G = np.stack([s.G for s in part])
@@ -157,7 +164,11 @@ def run_sims(sims: List[Sim], sc, empfcs, schedule=None, precision="f32", batch=
                         progress=progress)
         cols = res.columns()
         timings.append(dict(res.timings, sims=len(part)))
-        rows += [{c: float(cols[c][i]) for c in METRIC_COLS} for i in range(len(part))]
+        nan = np.full(len(part), np.nan)
+        new = [{c: float(cols.get(c, nan)[i]) for c in METRIC_COLS} for i in range(len(part))]
+        if on_batch is not None:
+            on_batch(part, new)
+        rows += new
         if want_fc:
             fcs += list(res.fc)
     run_sims.last_timings = timings
@@ -211,55 +222,118 @@ def gather_table(table, dist, device):
 
 
 def _rank_world():
+    """(rank, world, local rank, launcher).  torchrun: one process group over RCCL.
+    SLURM array (the reference's launcher, whole_sweep_both.py:23-24): independent
+    tasks with no process group; each writes only its own rank file and the table is
+    collapsed once every rank file is complete (`sweep collapse`, or the last task)."""
     if "WORLD_SIZE" in os.environ:
-        return int(os.environ.get("RANK", 0)), int(os.environ["WORLD_SIZE"]), int(os.environ.get("LOCAL_RANK", 0))
-    if "SLURM_ARRAY_TASK_ID" in os.environ:  # the reference's launcher (whole_sweep_both.py:23-24)
-        return int(os.environ["SLURM_ARRAY_TASK_ID"]), int(os.environ["SLURM_ARRAY_TASK_MAX"]) + 1, 0
-    return 0, 1, 0
+        return (int(os.environ.get("RANK", 0)), int(os.environ["WORLD_SIZE"]), int(os.environ.get("LOCAL_RANK", 0)),
+                "torch")
+    if "SLURM_ARRAY_TASK_ID" in os.environ:
+        return (int(os.environ["SLURM_ARRAY_TASK_ID"]), int(os.environ["SLURM_ARRAY_TASK_MAX"]) + 1,
+                int(os.environ.get("SLURM_LOCALID", 0)), "slurm")
+    return 0, 1, 0, "single"
+
+
+def _sim_list(args):
+    """The driver's simulation list and output tag (whole_sweep_both.py, _maps.py, run_many_seeds.py)."""
+    n = args.nodes
+    if args.kind == "homo":
+        sims = homogeneous(args.seeds or 50, args.seed0 or 0, args.grid, n)
+        tag = args.tag or f"sweep_delta_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_0_0" + (f"_N{n}" if n != 90 else "")
+    elif args.kind == "maps":
+        m1, m2 = args.map_ids
+        sims = maps(m1, m2, args.seeds or 25, 25 if args.seed0 is None else args.seed0, args.grid, n)
+        name = "deltaSHUFFLED" if (m1, m2) == (2, 2) else "deltamaps"
+        tag = args.tag or (f"sweep_{name}_from_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_{m1}_{m2}"
+                           + (f"_N{n}" if n != 90 else ""))
+    else:
+        sims = many_seeds(args.modality, args.seeds or 50, args.seed0 or 0, n)
+        tag = args.tag or f"run_50seeds_output_{args.modality}" + (f"_N{n}" if n != 90 else "")
+    if args.limit:
+        sims = sims[:args.limit]
+    return sims, tag
+
+
+def rank_files_complete(sims, out, tag, world):
+    """True when every rank's TSV file holds its whole round-robin shard."""
+    for r in range(world):
+        want = {(s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") for s in shard(sims, r, world)}
+        if not want <= done_keys(os.path.join(out, "temp", f"{tag}_rank{r}")):
+            return False
+    return True
+
+
+def collapse_sweep(sims, out, tag, world):
+    """{tag}.txt (the comma-separated table heatmaps.py reads) and {tag}_rows.npy, both
+    built from the rank files (so rows restored by a resumed run are included)."""
+    paths = [os.path.join(out, "temp", f"{tag}_rank{r}") for r in range(world)]
+    tmp = os.path.join(out, f".{tag}.txt.{os.getpid()}")
+    df = collapse(paths, tmp)
+    os.replace(tmp, os.path.join(out, f"{tag}.txt"))
+    index = {(s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}"): s for s in sims}
+    table = np.full((len(df), 4 + len(METRIC_COLS)), np.nan)
+    for i, r in enumerate(df.itertuples(index=False)):
+        s = index.get((int(r.seed), f"{r.delta_G:.4f}", f"{r.delta_sigma:.4f}"))
+        table[i, :4] = (r.rank, s.index if s else -1, r.seed, s.stream if s else -1)
+        table[i, 4:] = [getattr(r, c) for c in METRIC_COLS]
+    table = table[np.argsort(table[:, 1], kind="stable")]
+    np.save(os.path.join(out, f"{tag}_rows.npy"), table)
+    return table
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
-    ap.add_argument("kind", choices=("homo", "maps", "many"))
+    ap.add_argument("kind", choices=("homo", "maps", "many", "collapse"))
     ap.add_argument("--seeds", type=int, default=None)
     ap.add_argument("--seed0", type=int, default=None)
     ap.add_argument("--grid", default="shipped", choices=("shipped", "script"))
     ap.add_argument("--map-ids", type=int, nargs=2, default=(1, 1))
     ap.add_argument("--modality", default="map", choices=("homo", "map", "shuf"))
+    ap.add_argument("--nodes", type=int, default=90,
+                    help="90: the AAL connectome (SC_opti_25julio); other N: the synthetic connectome of "
+                         "BASELINE config 5 (datasets.synthetic_sc), no empirical FC so the gof columns are NaN")
     ap.add_argument("--out", default="output")
     ap.add_argument("--tag", default=None)
     ap.add_argument("--precision", default="f32", choices=("f32", "f64"))
     ap.add_argument("--batch", type=int, default=20_000)
     ap.add_argument("--short", action="store_true", help="short schedule (smoke runs): 0.02/0.2/20 s")
     ap.add_argument("--limit", type=int, default=None, help="only the first LIMIT simulations of the list")
+    ap.add_argument("--of", default="homo", choices=("homo", "maps"), help="collapse: which sweep's list")
+    ap.add_argument("--world", type=int, default=None, help="collapse: number of rank files")
     args = ap.parse_args(argv)
+
+    if args.kind == "collapse":  # SLURM-array runs: assemble the table once every rank file is complete
+        args.kind = args.of
+        sims, tag = _sim_list(args)
+        world = args.world or _rank_world()[1]
+        if not rank_files_complete(sims, args.out, tag, world):
+            raise SystemExit(f"collapse: the {world} rank files of {tag} are not complete yet")
+        collapse_sweep(sims, args.out, tag, world)
+        return
 
     import torch
     from .model import Schedule
-    rank, world, local = _rank_world()
+    rank, world, local, launcher = _rank_world()
     dist = None
+    if launcher == "slurm":
+        local %= max(1, torch.cuda.device_count())
     device = f"cuda:{local}"
-    if world > 1 and "WORLD_SIZE" in os.environ:
+    if launcher == "torch" and world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     os.makedirs(os.path.join(args.out, "temp"), exist_ok=True)
-    if args.kind == "homo":
-        sims = homogeneous(args.seeds or 50, args.seed0 or 0, args.grid)
-        tag = args.tag or f"sweep_delta_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_0_0"
-    elif args.kind == "maps":
-        m1, m2 = args.map_ids
-        sims = maps(m1, m2, args.seeds or 25, 25 if args.seed0 is None else args.seed0, args.grid)
-        name = "deltaSHUFFLED" if (m1, m2) == (2, 2) else "deltamaps"
-        tag = args.tag or f"sweep_{name}_from_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_{m1}_{m2}"
-    else:
-        sims = many_seeds(args.modality, args.seeds or 50, args.seed0 or 0)
-        tag = args.tag or f"run_50seeds_output_{args.modality}"
-    if args.limit:
-        sims = sims[:args.limit]
+    sims, tag = _sim_list(args)
     sched = Schedule(n_trans1=200, n_trans2=2000, n_sim=200_000) if args.short else Schedule()
-    empfcs = {s: datasets.load_empfc(s) for s in STATES}
-    sc = datasets.load_sc()
+    if args.nodes == 90:
+        empfcs = {s: datasets.load_empfc(s) for s in STATES}
+        sc = datasets.load_sc()
+    else:
+        empfcs = {}
+        sc = datasets.synthetic_sc(args.nodes)
+    from .pipeline import check_supported
+    check_supported(sc.shape[0], sched)  # fail before integrating, not in the epilogue
     mine = shard(sims, rank, world)
 
     if args.kind == "many":
@@ -267,40 +341,55 @@ def main(argv=None):
         rows, fcs = run_sims(mine, sc, empfcs, sched, args.precision, args.batch, device, want_fc=True)
         hma = HMA.integration_segregation_batch(fcs, device) if fcs else []
         save = {(s.seed, s.state): d for s, d in zip(mine, hma)}
-        with open(os.path.join(args.out, "temp", f"{tag}_rank{rank}.pickle"), "wb") as f:
+        part_path = os.path.join(args.out, "temp", f"{tag}_rank{rank}.pickle")
+        with open(part_path + ".tmp", "wb") as f:
             pickle.dump(save, f)
+        os.replace(part_path + ".tmp", part_path)
         if dist:
             parts = [None] * world
             dist.all_gather_object(parts, save)
+        elif launcher == "slurm":  # merge only once every task's part exists (our own files)
+            paths = [os.path.join(args.out, "temp", f"{tag}_rank{r}.pickle") for r in range(world)]
+            parts = None
+            if all(os.path.exists(p) for p in paths):
+                parts = []
+                for p in paths:
+                    with open(p, "rb") as f:
+                        parts.append(pickle.load(f))
         else:
             parts = [save]
-        if rank == 0:
+        if parts is not None and (rank == 0 or launcher == "slurm"):
             merged = {k: v for p in parts for k, v in p.items()}
             merged["metainfo"] = {st: sum(1 for k in merged if k != "metainfo" and k[1] == st) for st in STATES}
-            with open(os.path.join(args.out, f"{tag}.pickle"), "wb") as f:
+            final = os.path.join(args.out, f"{tag}.pickle")
+            with open(final + f".{os.getpid()}", "wb") as f:
                 pickle.dump(merged, f)
+            os.replace(final + f".{os.getpid()}", final)
     else:
         path = os.path.join(args.out, "temp", f"{tag}_rank{rank}")
         have = done_keys(path)
         todo = [s for s in mine if (s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") not in have]
         t0 = time.perf_counter()
-        rows, _ = run_sims(todo, sc, empfcs, sched, args.precision, args.batch, device, progress=Progress(rank))
+        rows, _ = run_sims(todo, sc, empfcs, sched, args.precision, args.batch, device, progress=Progress(rank),
+                           on_batch=lambda part, new: append_rows(path, rank, part, new))
         wall = time.perf_counter() - t0
         n_steps = len(todo) * sc.shape[0] * sched.n_total
-        perf = json.dumps({"rank": rank, "sims": len(todo), "wall_s": wall, "node_steps": n_steps,
-                           "node_steps_per_s": n_steps / wall if wall else None,
+        perf = json.dumps({"rank": rank, "sims": len(todo), "nodes": sc.shape[0], "wall_s": wall,
+                           "node_steps": n_steps, "node_steps_per_s": n_steps / wall if wall else None,
                            "batches": getattr(run_sims, "last_timings", None)})
         print(perf, flush=True)
         with open(os.path.join(args.out, "temp", f"{tag}_rank{rank}_perf.jsonl"), "a") as f:  # one line per run
             f.write(perf + "\n")
-        append_rows(path, rank, todo, rows)
-        table = rows_table(rank, todo, rows)
-        if dist:
-            table = gather_table(table, dist, torch.device(device))
-        if rank == 0:
-            paths = [os.path.join(args.out, "temp", f"{tag}_rank{r}") for r in range(world)]
-            collapse(paths, os.path.join(args.out, f"{tag}.txt"))
-            np.save(os.path.join(args.out, f"{tag}_rows.npy"), table)
+        gathered = None
+        if dist:  # every rank's rows reach rank 0 over RCCL (its rank file is flushed by then)
+            gathered = gather_table(rows_table(rank, todo, rows), dist, torch.device(device))
+        if launcher == "slurm":
+            if rank_files_complete(sims, args.out, tag, world):  # the last task to finish assembles
+                collapse_sweep(sims, args.out, tag, world)
+        elif rank == 0:
+            table = collapse_sweep(sims, args.out, tag, world)
+            if gathered is not None and not set(gathered[:, 1].astype(int)) <= set(table[:, 1].astype(int)):
+                raise RuntimeError("collapsed table is missing rows the ranks gathered")
     if dist:
         dist.barrier()
         dist.destroy_process_group()

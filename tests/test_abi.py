@@ -27,11 +27,21 @@ def test_library_exports_header_symbols():
         assert hasattr(lib, name), name
 
 
+def test_product_library_has_no_diagnostic_entry_points():
+    """The ablation entry point ships only in libwcsde_diag.so (csrc/wcsde_diag.h)."""
+    from nremmodfc_amd import _build
+    _build.build()
+    lib = ctypes.CDLL(_build.LIB)
+    assert not hasattr(lib, "wc_diag_integrate")
+    assert not hasattr(lib, "wc_large_diag")
+
+
 def test_abi_version_and_workspace():
     from nremmodfc_amd import _lib
     L = _lib.lib()
-    assert L.wcsde_abi_version() == 3
-    assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16   # bf16x6 image
+    assert L.wcsde_abi_version() == 4
+    # N <= 96: sized for the 3-part 16-bit image (the fp16x2 image and its two scale floats fit inside)
+    assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16
     assert L.wc_workspace_size(20000, 90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
     assert L.wc_workspace_size(1, 16, _lib.WC_F32) == 2 * 1 * 3 * 64 * 16
     # N > 96 (wc_sde_large.hip): fp16x2 A image + 2 scale floats (one 256-B slot) + 6 fp32 state arrays
@@ -62,7 +72,14 @@ def test_invalid_arguments_fail_loudly():
     cfg = _lib.WCBoldCfgC()
     cfg.dec, cfg.neq, cfg.n_total = 1000, 2000, 2010  # fewer than neq + 16 samples
     assert L.wc_bold_init(ctypes.byref(cfg), 10, ctypes.c_void_p(16), None) == -1
-    assert L.wc_fc_metrics(1, 200, 298, None, None, None, 0, 1.0, None, None, None, None, None) == -1
+    assert L.wc_fc_metrics(1, 200, 298, None, None, None, 0, 1.0, None, None, None, None, None, 0, None) == -1
+    vp = ctypes.c_void_p(16)
+    assert L.wc_fc_metrics_workspace_size(4, 90, 298, 4, 0) == 0           # N <= 96: LDS only
+    need = L.wc_fc_metrics_workspace_size(4, 1000, 298, 0, 0)             # N > 96: the FC tiles in global memory
+    assert need >= 4 * 1000 * 1000 * 8
+    assert L.wc_fc_metrics_workspace_size(4, 1000, 298, 0, 1) < need - 4 * 1000 * 1000 * 8 + 1
+    assert L.wc_fc_metrics(4, 1000, 298, vp, None, None, 0, 1.0, None, None, None, vp, vp, need - 8, None) == -3
+    assert L.wc_fc_metrics(4, 6, 298, vp, None, None, 0, 1.0, None, None, None, vp, None, 0, None) == -1
     assert L.wc_kuramoto(0, 90, 298, None, None, None) == -1
     assert L.wc_welch_bins() == 2001
 
@@ -82,7 +99,9 @@ def test_corrcoef_validates_without_device_work():
     vp = ctypes.c_void_p(16)
     assert L.wc_corrcoef_workspace_size(10, 90, 6000) > 10 * 90 * 90 * 8
     assert L.wc_corrcoef_workspace_size(0, 90, 6000) == 0
-    assert L.wc_corrcoef(10, 97, 6000, vp, vp, vp, 1 << 30, None) == -1  # N > 96
+    assert L.wc_corrcoef_workspace_size(10, 1000, 6000) == 2 * 10 * 1000 * 8  # N > 96: means and sds
+    assert L.wc_corrcoef(10, 1000, 6000, vp, vp, vp, 64, None) == -3        # N > 96 workspace
+    assert L.wc_corrcoef(10, 1, 6000, vp, vp, vp, 1 << 30, None) == -1       # N < 2
     assert L.wc_corrcoef(10, 90, 1, vp, vp, vp, 1 << 30, None) == -1     # M < 2
     assert L.wc_corrcoef(10, 90, 6000, vp, vp, vp, 64, None) == -3       # workspace
     assert b"workspace" in L.wc_last_error()

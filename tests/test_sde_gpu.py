@@ -69,6 +69,13 @@ def tol(prec):
     return (1e-9, 1e-10) if prec == "f64" else (2e-3, 2e-4)
 
 
+def observed(d, tag):
+    """Print the observed max / rms deviation (the tolerances are set from these)."""
+    mx, rms = float(d.max()), float(np.sqrt(np.mean(d ** 2)))
+    print(f"TOL {tag} max={mx:.3e} rms={rms:.3e}", flush=True)
+    return mx, rms
+
+
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 def test_homogeneous_sweep_cells(cuda, sc90, prec):
     """16 cells of the shipped (dG, dsigma) grid, 2 seeds each = 2 waves + a tail of 5."""
@@ -81,6 +88,7 @@ def test_homogeneous_sweep_cells(cuda, sc90, prec):
     g, o, gb, ob, _ = run_pair(sc90, G, S, keys, 300, 300, 600, 20, prec)
     mx, rms = tol(prec)
     d = np.abs(g - o)
+    observed(d, f"homo-{prec}")
     assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
     for x, y in ((gb.E, ob.E), (gb.I, ob.I), (gb.A, ob.A)):
         dd = np.abs(x.cpu().numpy() - y)
@@ -100,6 +108,7 @@ def test_maps_heterogeneous_params(cuda, sc90, prec):
     g, o, *_ = run_pair(sc90, G, S, keys, 200, 200, 400, 20, prec)
     mx, rms = tol(prec)
     d = np.abs(g - o)
+    observed(d, f"maps-{prec}")
     assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
 
 
@@ -147,6 +156,7 @@ def test_f32_tracks_f64_statistics(cuda, sc90):
         rec = torch.empty((2500, 16, 90), dtype=b.rec_dtype, device="cuda")
         b.integrate(50_000, 2.0, 20, rec)
         out[prec] = rec.double().mean(0).cpu().numpy()
+    observed(np.abs(out["f32"] - out["f64"]), "f32-vs-f64-mean-100k")
     assert np.abs(out["f32"] - out["f64"]).max() < 0.02
 
 
@@ -174,6 +184,7 @@ def test_grouped_kernel_matches_register_kernel(cuda, sc90, B):
     ob.integrate(100, 0.05)
     o = ob.integrate(300, 2.0, 20)
     d = np.abs(rb[:, -24:].double().cpu().numpy().transpose(1, 0, 2) - o)
+    observed(d, f"grouped-{B}")
     assert d.max() <= 2e-3 and np.sqrt(np.mean(d ** 2)) <= 2e-4
 
 
@@ -213,4 +224,5 @@ def test_f32_shapes_and_tails(cuda, N, B):
     keys = sim_keys(list(range(B)), [N] * B)
     g, o, *_ = run_pair(sc, 0.16, 7.68, keys, 100, 0, 200, 20, "f32")
     d = np.abs(g - o)
+    observed(d, f"shapes-{N}-{B}")
     assert d.max() <= 2e-3 and np.sqrt(np.mean(d ** 2)) <= 2e-4, (d.max(), np.sqrt(np.mean(d ** 2)))

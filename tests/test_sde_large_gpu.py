@@ -13,7 +13,7 @@ import torch
 import oracle
 from nremmodfc_amd import datasets
 from nremmodfc_amd.model import Batch, driver_params, sim_keys
-from tests.test_sde_gpu import run_pair, tol
+from tests.test_sde_gpu import observed, run_pair, tol
 
 pytestmark = pytest.mark.gpu
 
@@ -34,6 +34,7 @@ def test_large_vs_oracle(cuda, prec, N, B):
     g, o, gb, ob, _ = run_pair(sc, G, S, keys, n // 2, n // 2, n, 7, prec)
     mx, rms = tol(prec)
     d = np.abs(g - o)
+    observed(d, f"large-{prec}-{N}-{B}")
     assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
     for x, y in ((gb.E, ob.E), (gb.I, ob.I), (gb.A, ob.A)):
         assert np.abs(x.cpu().numpy() - y).max() <= mx
@@ -82,4 +83,5 @@ def test_large_f32_tracks_f64_statistics(cuda):
         rec = torch.empty((200, B, N), dtype=b.rec_dtype, device="cuda")
         b.integrate(4000, 2.0, 20, rec)
         out[prec] = rec.double().mean(0).cpu().numpy()
+    observed(np.abs(out["f32"] - out["f64"]), "large-f32-vs-f64-mean")
     assert np.abs(out["f32"] - out["f64"]).max() < 0.02

@@ -173,3 +173,80 @@ def test_many_seeds_main_short(tmp_path, cuda):
         np.testing.assert_allclose(d[k]["Hin_sim"], h["Hin_sim"], rtol=1e-12)
         np.testing.assert_allclose(d[k]["Hse_sim"], h["Hse_sim"], rtol=1e-11)
         np.testing.assert_allclose(d[k]["Hse_node_sim"], h["Hse_node_sim"], rtol=1e-9, atol=1e-15)
+
+
+def _write_rank_files(out, tag, sims, world, ranks):
+    os.makedirs(os.path.join(out, "temp"), exist_ok=True)
+    for r in ranks:
+        mine = sweep.shard(sims, r, world)
+        rows = [{c: s.index + 0.001 * j for j, c in enumerate(sweep.METRIC_COLS)} for s in mine]
+        sweep.append_rows(os.path.join(out, "temp", f"{tag}_rank{r}"), r, mine, rows)
+
+
+def test_collapse_waits_for_every_rank_file(tmp_path):
+    """SLURM-array runs (no process group): the table is assembled only once every
+    rank file holds its whole shard; rows.npy comes from the rank files (resumed rows included)."""
+    out = str(tmp_path)
+    sims = sweep.homogeneous(1)[:7]
+    _write_rank_files(out, "c", sims, 2, [0])
+    argv = ["collapse", "--of", "homo", "--seeds", "1", "--limit", "7", "--world", "2", "--out", out, "--tag", "c"]
+    with pytest.raises(SystemExit):
+        sweep.main(argv)
+    assert not os.path.exists(os.path.join(out, "c.txt"))
+    _write_rank_files(out, "c", sims, 2, [1])
+    sweep.main(argv)
+    import pandas as pd
+    df = pd.read_csv(os.path.join(out, "c.txt"))
+    assert len(df) == 7 and list(df.columns) == sweep.HEADER
+    rows = np.load(os.path.join(out, "c_rows.npy"))
+    np.testing.assert_array_equal(rows[:, 1], np.arange(7))
+    np.testing.assert_array_equal(rows[:, 0], np.arange(7) % 2)
+    np.testing.assert_allclose(rows[:, 4], np.round(np.arange(7), 4))
+
+
+def test_slurm_rank_world(monkeypatch):
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("SLURM_ARRAY_TASK_ID", "3")
+    monkeypatch.setenv("SLURM_ARRAY_TASK_MAX", "7")
+    monkeypatch.setenv("SLURM_LOCALID", "1")
+    assert sweep._rank_world() == (3, 8, 1, "slurm")
+
+
+def test_n1000_sim_lists_use_synthetic_maps():
+    sims = sweep.maps(1, 1, n_iterations=1, n_init=0, n=1000)
+    assert sims[0].G.shape == (1000,) and abs(sims[0].G.mean() - (0.16 + sims[0].dG)) < 1e-12
+    shuf = sweep.maps(2, 2, n_iterations=1, n_init=0, n=1000)
+    assert sorted(shuf[5].G) == pytest.approx(sorted(sims[5].G))
+    assert not np.array_equal(shuf[5].G, sims[5].G)
+
+
+@pytest.mark.gpu
+def test_slurm_array_two_tasks(tmp_path, cuda, monkeypatch):
+    """Two SLURM-array tasks run one after the other: the first writes only its rank
+    file, the second (finding every rank file complete) assembles the table."""
+    import pandas as pd
+    out = str(tmp_path)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setenv("SLURM_ARRAY_TASK_MAX", "1")
+    argv = ["homo", "--seeds", "1", "--short", "--limit", "5", "--out", out, "--tag", "s"]
+    monkeypatch.setenv("SLURM_ARRAY_TASK_ID", "1")
+    sweep.main(argv)
+    assert os.path.exists(os.path.join(out, "temp", "s_rank1")) and not os.path.exists(os.path.join(out, "s.txt"))
+    monkeypatch.setenv("SLURM_ARRAY_TASK_ID", "0")
+    sweep.main(argv)
+    df = pd.read_csv(os.path.join(out, "s.txt"))
+    assert sorted(df["rank"]) == [0, 0, 0, 1, 1] and np.isfinite(df[sweep.METRIC_COLS].to_numpy()).all()
+
+
+@pytest.mark.gpu
+def test_sweep_main_n1000_short(tmp_path, cuda):
+    """Config 5 through the driver: the synthetic 1000-node connectome, no empirical FC
+    (gof columns NaN), FC-derived columns and the Welch peak written."""
+    import pandas as pd
+    out = str(tmp_path)
+    sweep.main(["homo", "--seeds", "1", "--short", "--limit", "3", "--nodes", "1000", "--out", out, "--tag", "n"])
+    df = pd.read_csv(os.path.join(out, "n.txt"))
+    assert len(df) == 3 and list(df.columns) == sweep.HEADER
+    assert df[[c for c in sweep.METRIC_COLS if c[:4] in ("ssim", "corr") or c[0] == "e"]].isna().all().all()
+    good = df[["sync", "meta", "mean", "peakfreq"]].to_numpy()
+    assert np.isfinite(good).all() and (df["peakfreq"] > 0).all()

@@ -15,7 +15,10 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+# the ablation entry point lives in the diag build only (python -m nremmodfc_amd._build --diag)
+os.environ.setdefault("WCSDE_LIB_OVERRIDE", os.path.join(ROOT, "nremmodfc_amd", "libwcsde_diag.so"))
 import oracle  # noqa: E402
 from bench import sweep_batch  # noqa: E402
 from nremmodfc_amd import _lib, datasets  # noqa: E402

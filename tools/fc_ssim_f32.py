@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Fixed-seed FC SSIM of the fp32 product pipeline over the full 1001 s schedule
+(298 BOLD samples), north_star "FC SSIM >= 0.999 vs reference" with utils.py:48's
+data_range = 1.  The reference at fixed seed is the fp64 pipeline (pinned to the
+oracle at <= 1e-9 on short horizons and FC SSIM >= 0.999999 at 400k steps).
+
+Prints: per-seed SSIM(fp32 FC, fp64 FC) at the same seed; the between-seed floor
+SSIM(fp64 FC seed s, fp64 FC seed s+1); SSIM of the seed-averaged FCs (fp32 mean vs
+fp64 mean) and the split-half floor of that (fp64 seeds 0..B/2-1 vs B/2..B-1).
+
+  python tools/fc_ssim_f32.py [B] [n_sim]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import oracle.sigchain as osg  # noqa: E402
+from nremmodfc_amd import datasets, sweep  # noqa: E402
+from nremmodfc_amd.model import Schedule, sim_keys  # noqa: E402
+from nremmodfc_amd.pipeline import run_sweep  # noqa: E402
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+    n_sim = int(sys.argv[2]) if len(sys.argv) > 2 else 6_000_000
+    sims = [s for s in sweep.homogeneous(B, 0) if (round(s.dG, 4), round(s.dsigma, 4)) == (0.0, 0.0)]
+    sc = datasets.load_sc()
+    emp = {s: datasets.load_empfc(s) for s in datasets.STATES}
+    G = np.stack([s.G for s in sims])
+    S = np.stack([s.sigma for s in sims])
+    keys = sim_keys([s.seed for s in sims], [s.stream for s in sims])
+    sch = Schedule(n_sim=n_sim)
+    res, wall = {}, {}
+    for prec in ("f32", "f64"):
+        t = time.perf_counter()
+        res[prec] = run_sweep(sc, G, S, keys, emp, sch, precision=prec, want_fc=True)
+        wall[prec] = time.perf_counter() - t
+    f32, f64 = res["f32"].fc, res["f64"].fc
+    same = np.array([osg.ssim(f32[b], f64[b], 1.0) for b in range(B)])
+    floor = np.array([osg.ssim(f64[b], f64[(b + 1) % B], 1.0) for b in range(B)])
+    mean_ssim = osg.ssim(f32.mean(0), f64.mean(0), 1.0)
+    half = osg.ssim(f64[:B // 2].mean(0), f64[B // 2:].mean(0), 1.0)
+    c32, c64 = res["f32"].columns(), res["f64"].columns()
+    out = {"B": B, "n_sim": n_sim, "bold_samples": (n_sim // 20 - 2000 + 999) // 1000,
+           "same_seed_ssim": {"mean": same.mean(), "min": same.min(), "max": same.max()},
+           "between_seed_ssim": {"mean": floor.mean(), "min": floor.min(), "max": floor.max()},
+           "seed_mean_fc_ssim_f32_vs_f64": mean_ssim, "split_half_floor_f64": half,
+           "peakfreq_equal_frac": float(np.mean(c32["peakfreq"] == c64["peakfreq"])),
+           "column_means_f32": {k: float(np.mean(v)) for k, v in c32.items()},
+           "column_means_f64": {k: float(np.mean(v)) for k, v in c64.items()},
+           "wall_s": wall}
+    print(json.dumps(out, default=float), flush=True)
+
+
+if __name__ == "__main__":
+    main()
