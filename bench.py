@@ -13,7 +13,9 @@ chunks of 20,000 Euler steps of the recorded phase (tau_ip = 2, E stored every
 the sweep pipeline (nremmodfc_amd/pipeline.py); inputs and state resident in
 HBM.  --sde-only times the integrator alone.  With --gpus N (torchrun, one rank per
 GPU) each rank runs its own 20,000-simulation shard (seeds 50r..50r+49):
-weak scaling, no data-path collective.
+weak scaling, no data-path collective.  --scaling strong instead splits the ONE
+20,000-simulation C3 sweep over the ranks with the reference's round robin
+(simulation i on rank i % N, whole_sweep_both.py:63-64).
 
 Prints ONE JSON line (rank 0).
 """
@@ -63,14 +65,17 @@ def sweep_batch(rank, n_seeds=50, nG=20, nS=20):
     return G, S, keys
 
 
+CPU_SHARE = 16  # host cores one GPU's job may use on the GPU box (its OMP_NUM_THREADS / MAX_JOBS)
+
+
 def cpu_baseline(sc, seconds=15.0, steps=2000):
     """The oracle's C restatement of run() on the host cores (kind 'port')."""
     import oracle
     try:
-        ncores = len(os.sched_getaffinity(0))
+        avail = len(os.sched_getaffinity(0))
     except AttributeError:
-        ncores = os.cpu_count()
-    ncores = max(1, min(ncores, 16))   # the box's CPU share for one GPU
+        avail = os.cpu_count()
+    ncores = max(1, min(avail, CPU_SHARE))
     G, S, keys = sweep_batch(0)
     p = driver_params()
     B = 2 * ncores
@@ -85,6 +90,7 @@ def cpu_baseline(sc, seconds=15.0, steps=2000):
             break
     ns = B * sc.shape[0] * steps * n
     return {"value": ns / total, "unit": "node-timesteps/sec", "cores": ncores, "kind": "port",
+            "cores_available": avail, "cores_cap": CPU_SHARE,
             "sample": f"{B} sims x {steps * n} Euler steps of the C3 grid (tau_ip=2, E recorded every "
                       f"20 steps), oracle/wc_oracle.c fp64, OpenMP over simulations, {total:.1f} s"}
 
@@ -104,6 +110,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="weak: 20,000 (c3) / 2,500 (c5) sims per rank; strong: the one c3 sweep (20,000 sims) or "
+                         "c5 sweep (20,000 sims over 8 GPUs = 2,500 x 8) split round-robin over the ranks")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,7 +131,14 @@ def main():
 
     from nremmodfc_amd.sigchain import NEQ, BoldStream, WelchAccumulator
 
-    if args.config == "c5":
+    if args.scaling == "strong":  # one sweep, the reference's round robin (whole_sweep_both.py:63-64)
+        G, S, keys = sweep_batch(0)
+        if args.config == "c5":  # the C5 job: 20,000 sims over 8 GPUs; strong scaling of 1/8 of it per GPU at N=8
+            G, S, keys = G[:2500 * 8], S[:2500 * 8], keys[:2500 * 8]
+        mine = np.arange(len(keys)) % world == rank
+        G, S, keys = G[mine], S[mine], keys[mine]
+        sc = datasets.synthetic_sc(1000) if args.config == "c5" else datasets.load_sc()
+    elif args.config == "c5":
         sc = datasets.synthetic_sc(1000)
         G, S, keys = sweep_batch(rank)
         lo = rank * 2500 % len(keys)
@@ -201,25 +217,70 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern = {k: (sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None) for k, v in ev.items()}
-    node_steps = B * N * EULER * CHUNKS * args.steps * world
+    B_all = B
+    if dist:  # strong scaling: shards may differ by one simulation
+        t = torch.tensor([B], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.int64)
+        dist.all_reduce(t)
+        B_all = int(t.item())
+    else:
+        B_all = B * world
+    node_steps = B_all * N * EULER * CHUNKS * args.steps
     value = node_steps / elapsed
     fl = flops_per_node_step(N)
-    peak = PEAK_FP32_TFLOPS if args.precision == "f32" else PEAK_FP64_TFLOPS
     per_launch_ns = B * N * EULER
-    achieved = per_launch_ns * fl / (kern["sde"] * 1e-3) / 1e12
-    traffic = None
-    util = {}
+    t_launch = kern["sde"] * 1e-3
+    pmc_d = {}
     pmc = os.path.join(ROOT, "profiles", "pmc_sde.json" if args.config == "c3" else "pmc_sde_c5.json")
     if os.path.exists(pmc):
         try:
             d = json.load(open(pmc))
             if d.get("B") == B and d.get("N") == N and d.get("euler_steps") == EULER and \
                     d.get("precision") == args.precision:
-                traffic = d.get("hbm_bytes_per_launch")
-                util = {k: d[k] for k in ("valu_insts_per_wave_step", "mfma_insts_per_wave_step", "mfma_busy_frac")
-                        if k in d}
+                pmc_d = d
         except (ValueError, OSError):
-            traffic = None
+            pmc_d = {}
+    traffic = pmc_d.get("hbm_bytes_per_launch")
+    util = {k: pmc_d[k] for k in ("valu_insts_per_wave_step", "mfma_insts_per_wave_step", "mfma_busy_frac")
+            if k in pmc_d}
+    sq = pmc_d.get("sq", {})
+    if sq.get("SQ_ACTIVE_INST_VALU") and sq.get("GRBM_GUI_ACTIVE"):
+        # SQ_ACTIVE_INST_VALU counts quad-cycles per SIMD; GRBM_GUI_ACTIVE sums the 8 XCDs' clocks
+        util["valu_issue_busy_frac"] = 4 * sq["SQ_ACTIVE_INST_VALU"] / (sq["GRBM_GUI_ACTIVE"] / 8 * 1024)
+    issued = None
+    if args.precision == "f32":
+        ifl = issued_mfma_flops_per_node_step(N)
+        issued = {"dtype": "f16", "flops_per_node_step": ifl, "tflops": per_launch_ns * ifl / t_launch / 1e12,
+                  "peak": PEAK_F16_TFLOPS, "util": per_launch_ns * ifl / t_launch / 1e12 / PEAK_F16_TFLOPS}
+    if N <= 96:
+        # C3 (wc_sde_kernel): state in registers for the whole launch; PMC: VALU-issue-bound (MFMA busy ~15 %).
+        # SURVEY 8(d)'s algorithmic work F(N) = 2N + 35 flops per node-step against the fp32 VECTOR (VALU) peak.
+        peak = PEAK_FP32_TFLOPS if args.precision == "f32" else PEAK_FP64_TFLOPS
+        achieved = per_launch_ns * fl / t_launch / 1e12
+        roof = {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                "traffic": traffic, "traffic_algorithmic": B * N * (EULER // R * 4 + 2 * 3 * 8 + 2 * 8),
+                "kernel": "wc_sde_kernel (one launch = %d Euler steps of %d sims)" % (EULER, B),
+                "algorithmic_flops_per_node_step": fl,
+                "note": "bound from PMC: VALU issue (pmc.valu_issue_busy_frac); the coupling runs on the fp16 "
+                        "MFMA (issued_mfma) beside it. frac = algorithmic flops / fp32 vector peak"}
+        # SURVEY.md 8(d)'s state-streaming price (24 B per node-step) for the north star's "HBM roofline"
+        # wording: a register-resident integrator moves none of it, so the ratio is not a roofline fraction
+        gbps = per_launch_ns * 24 / t_launch / 1e9
+        roof["state_streaming_equiv"] = {"bytes_per_node_step": 24, "GBps": gbps, "x_hbm_peak": gbps / PEAK_HBM_GBPS}
+    else:
+        # C5 (step_kernel): one launch per Euler step, the state streams through HBM / Infinity Cache each
+        # step -- priced against HBM at the algorithmic 24 B per node-step (fp32 E, I, a_ie read + written)
+        achieved = per_launch_ns * 24 / t_launch / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_algorithmic": per_launch_ns * 24,
+                "kernel": "step_kernel (wc_sde_large.hip; %d launches of 1 Euler step, %d sims)" % (EULER, B),
+                "algorithmic_bytes_per_node_step": 24,
+                "algorithmic_flops_per_node_step": fl,
+                "algorithmic_tflops_fp32_equiv": per_launch_ns * fl / t_launch / 1e12,
+                "note": "traffic = PMC FETCH+WRITE per launch (includes Infinity-Cache hits): the kernel moves "
+                        "36 B of state per node-step plus the per-XCD connectome and E-image fetches"}
+    roof["kernel_ms_per_launch"] = kern["sde"]
+    roof["pmc"] = util or None
+    roof["issued_mfma"] = issued
     out = {
         "metric": "node-timesteps/sec (90-node WC, (G,sigma)x50-seed sweep) at 1/2/4/8 GPUs"
                   + ("" if args.config == "c3" else " [config 5: 1000-node synthetic connectome]"),
@@ -230,9 +291,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "f32" if args.precision == "f32" else "f64",
+        "dtype": "f32 (fp16x3 22-bit coupling)" if args.precision == "f32" else "f64",
+        "dtype_detail": ("E, I, sigmoids fp32; CM.E on the fp16 MFMA as three cross terms of two-part fp16 "
+                         "(22-bit) operands with fp32 accumulation; a_ie a compensated fp32 pair"
+                         if args.precision == "f32" else "fp64 throughout (fp64 MFMA coupling)"),
         "data": "synthetic noise (Philox), " + ("real 90-node SC_opti_25julio connectome" if args.config == "c3"
                                                 else "synthetic 1000-node connectome (datasets.synthetic_sc)"),
         "config": {"workload": ("C3: full homogeneous (G,sigma) sweep x 50 seeds (whole_sweep_both.py) per GPU; "
@@ -241,31 +305,9 @@ def main():
                                + "one step = 2000 recorded samples (40,000 Euler steps, tau_ip=2) of every simulation"
                                + ("" if args.sde_only else
                                   " + streamed BOLD/band-pass of both 1000-sample chunks + one Welch segment"),
-                   "sims_per_gpu": B, "nodes": N, "euler_steps_per_step": EULER * CHUNKS,
-                   "record_every": R, "parallelism": f"sims sharded x{world}"},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                     "frac": achieved / peak, "traffic": traffic,
-                     "traffic_algorithmic": B * N * (EULER // R * 4 + 2 * 3 * 8 + 2 * 8),
-                     "kernel": ("wc_sde_kernel (one launch = %d Euler steps of %d sims)" % (EULER, B) if N <= 96 else
-                                "step_kernel (wc_sde_large.hip; %d launches of 1 Euler step, %d sims)" % (EULER, B)),
-                     "kernel_ms_per_launch": kern["sde"],
-                     "flops_per_node_step": fl,
-                     "pmc": util or None,
-                     # the north star's "HBM roofline" wording, priced as a state-streaming
-                     # integrator would run (fp32 E, I, a_ie read + written per node-step = 24 B); this
-                     # kernel keeps the state in registers, so the fraction can exceed 1
-                     "hbm_state_streaming_equiv": {"bytes_per_node_step": 24,
-                                                   "GBps": per_launch_ns * 24 / (kern["sde"] * 1e-3) / 1e9,
-                                                   "peak_GBps": PEAK_HBM_GBPS,
-                                                   "frac": per_launch_ns * 24 / (kern["sde"] * 1e-3) / 1e9
-                                                   / PEAK_HBM_GBPS},
-                     "issued_mfma": ({"dtype": "f16", "flops_per_node_step": issued_mfma_flops_per_node_step(N),
-                                      "tflops": per_launch_ns * issued_mfma_flops_per_node_step(N)
-                                      / (kern["sde"] * 1e-3) / 1e12,
-                                      "peak": PEAK_F16_TFLOPS,
-                                      "frac": per_launch_ns * issued_mfma_flops_per_node_step(N)
-                                      / (kern["sde"] * 1e-3) / 1e12 / PEAK_F16_TFLOPS}
-                                     if args.precision == "f32" else None)},
+                   "sims_per_gpu": B, "sims_total": B_all, "nodes": N, "euler_steps_per_step": EULER * CHUNKS,
+                   "record_every": R, "parallelism": f"sims sharded x{world} ({args.scaling} scaling)"},
+        "roofline": roof,
         "kernel_ms": kern,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":

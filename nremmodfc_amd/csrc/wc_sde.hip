@@ -650,8 +650,11 @@ int cu_count() {
     return n;
 }
 
-// 81 <= N <= 96 (NT = 6).  Few groups of 16 sims: the register-resident product
-// kernel (connectome fragments in VGPRs, 214 registers, 2 workgroups per CU).
+// 81 <= N <= 96 (NT = 6).  Few groups of 16 sims (B <= 8192: the per-GPU shards of a
+// strong-scaled sweep): the register-resident kernel with SIX waves per group, one node
+// tile each (connectome fragments in VGPRs) -- the step is latency-bound there, and one
+// tile per wave halves each wave's dependent chain (2,500 sims: 1.06 -> 0.83 us per step,
+// tools/time_small.py); the per-tile arithmetic is the 3-wave kernel's, bit for bit.
 // Many groups: ONE workgroup per CU holding SG = ceil(groups / CUs) groups that
 // share the LDS connectome image (<= 155 / 128 registers): every simulation is
 // resident at once (a single round of workgroups, no tail) at 3-4 waves/SIMD.
@@ -659,7 +662,7 @@ int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) 
     constexpr int V = V_F16X3 | V_KAHAN_A;
     const int groups = (ka.B + kSims - 1) / kSims;
     const int cus = cu_count();
-    if (groups <= 2 * cus) return launch_v<float, 6, 3, kVarF32>(ka, sc, ws, st);
+    if (groups <= 2 * cus) return launch_v<float, 6, 6, kVarF32>(ka, sc, ws, st);
     // node-major E-only recording (the sweep pipeline's ring): pairs of records per 8-B store
     const bool rec2 = ka.rec_every > 0 && ka.rec_ld > 0 && ka.rec_ld % 2 == 0 && !ka.recI && !ka.recA &&
                       ((uintptr_t)ka.recE & 7) == 0;

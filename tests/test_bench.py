@@ -21,6 +21,7 @@ def test_cpu_baseline_leg():
     cb = bench.cpu_baseline(datasets.load_sc(), seconds=0.3, steps=200)
     assert cb["kind"] == "port" and cb["unit"] == "node-timesteps/sec"
     assert cb["value"] > 0 and 1 <= cb["cores"] <= 16 and "oracle/wc_oracle.c" in cb["sample"]
+    assert cb["cores"] == min(cb["cores_available"], cb["cores_cap"])
 
 
 @pytest.mark.gpu
@@ -36,12 +37,24 @@ def test_bench_json_contract(cuda):
         assert k in d, k
     assert d["metric"].startswith("node-timesteps/sec") and d["unit"] == "node-timesteps/sec"
     assert d["n_gpus"] == 1 and d["steps"] == 1 and d["warmup"] == 1 and d["higher_is_better"] is True
-    assert d["scaling"] == "weak" and d["vs_baseline"] is None and d["dtype"] == "f32"
+    assert d["scaling"] == "weak" and d["vs_baseline"] is None and d["dtype"].startswith("f32")
     assert "workload" in d["config"] and d["config"]["sims_per_gpu"] == 20000
     # value = node-steps of the timed steps / wall time
     ns = d["config"]["sims_per_gpu"] * d["config"]["nodes"] * d["config"]["euler_steps_per_step"] * d["steps"]
     assert abs(ns / (d["ms_per_step"] * 1e-3 * d["steps"]) / d["value"] - 1) < 1e-6
     r = d["roofline"]
-    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    assert r["bound"] == "valu" and r["unit"] == "TFLOP/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    assert "frac" not in r["state_streaming_equiv"]
     assert 0 < r["frac"] < 1.2 and r["issued_mfma"]["dtype"] == "f16"
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_c5_line_priced_on_hbm(cuda):
+    out = subprocess.run([sys.executable, "bench.py", "--config", "c5", "--steps", "1", "--warmup", "0",
+                          "--sde-only"], cwd=ROOT, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
+    assert d["config"]["nodes"] == 1000 and d["config"]["sims_per_gpu"] == 2500

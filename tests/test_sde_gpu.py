@@ -5,8 +5,11 @@ Tolerances (north_star: "within a stated fp64->fp32 tolerance at fixed seed"):
   * noise, fp32: |dz| <= 2e-3 worst case (v_log_f32 near u=1 feeds a sqrt),
     rms <= 2e-6;
   * trajectories over the short horizons below, fp64: max |dE| <= 1e-9;
-  * fp32 (E, I, coupling in fp32, a_ie in fp64): max |dE| <= 2e-3 and
-    rms <= 2e-4 over the same horizons.
+  * fp32 product path (fp32 E, I; fp16x3 22-bit coupling; a_ie a compensated fp32
+    pair): per test about 10x the deviation observed on MI355X (printed as "TOL ..."
+    lines; round-2 values in the comments), e.g. max 3e-4 / rms 1e-5 over the
+    1200-step sweep-cell horizon, 2e-6 / 3e-7 over 300 steps.  The deviation grows
+    with the horizon (the SDE is chaotic: DESIGN.md 4), so each test states its own.
 """
 import ctypes
 
@@ -65,8 +68,9 @@ def run_pair(sc, G, sig, keys, n1, n2, n3, rec_every, prec, params=None):
     return g, orec, gb, ob, recI
 
 
-def tol(prec):
-    return (1e-9, 1e-10) if prec == "f64" else (2e-3, 2e-4)
+def tol(prec, f32=(2e-3, 2e-4)):
+    """(max, rms) bound on |dE|: fp64 fixed; fp32 the caller's horizon-specific bound."""
+    return (1e-9, 1e-10) if prec == "f64" else f32
 
 
 def observed(d, tag):
@@ -86,7 +90,7 @@ def test_homogeneous_sweep_cells(cuda, sc90, prec):
     S = np.array([7.68 + b for a, b in cells] * 2 + [7.68] * 5)
     keys = sim_keys([0] * 16 + [1] * 16 + [2] * 5, list(range(16)) * 2 + [0] * 5)
     g, o, gb, ob, _ = run_pair(sc90, G, S, keys, 300, 300, 600, 20, prec)
-    mx, rms = tol(prec)
+    mx, rms = tol(prec, (3e-4, 1e-5))  # observed f32: max 2.7e-5, rms 1.0e-6 (1200 steps)
     d = np.abs(g - o)
     observed(d, f"homo-{prec}")
     assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
@@ -106,7 +110,7 @@ def test_maps_heterogeneous_params(cuda, sc90, prec):
     S = np.stack([7.68 + b * na for a in dGs for b in dss])
     keys = sim_keys(list(range(16)), [7] * 16)
     g, o, *_ = run_pair(sc90, G, S, keys, 200, 200, 400, 20, prec)
-    mx, rms = tol(prec)
+    mx, rms = tol(prec, (5e-5, 3e-6))  # observed f32: max 5.3e-6, rms 2.8e-7 (800 steps)
     d = np.abs(g - o)
     observed(d, f"maps-{prec}")
     assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
@@ -157,7 +161,7 @@ def test_f32_tracks_f64_statistics(cuda, sc90):
         b.integrate(50_000, 2.0, 20, rec)
         out[prec] = rec.double().mean(0).cpu().numpy()
     observed(np.abs(out["f32"] - out["f64"]), "f32-vs-f64-mean-100k")
-    assert np.abs(out["f32"] - out["f64"]).max() < 0.02
+    assert np.abs(out["f32"] - out["f64"]).max() < 5e-3  # observed 6.6e-4
 
 
 @pytest.mark.parametrize("B", [9000, 20000])
@@ -185,7 +189,7 @@ def test_grouped_kernel_matches_register_kernel(cuda, sc90, B):
     o = ob.integrate(300, 2.0, 20)
     d = np.abs(rb[:, -24:].double().cpu().numpy().transpose(1, 0, 2) - o)
     observed(d, f"grouped-{B}")
-    assert d.max() <= 2e-3 and np.sqrt(np.mean(d ** 2)) <= 2e-4
+    assert d.max() <= 3e-5 and np.sqrt(np.mean(d ** 2)) <= 3e-6  # observed max 3.4e-6, rms 2.9e-7 (400 steps)
 
 
 @pytest.mark.parametrize("nsteps", [400, 380, 20])
@@ -225,4 +229,5 @@ def test_f32_shapes_and_tails(cuda, N, B):
     g, o, *_ = run_pair(sc, 0.16, 7.68, keys, 100, 0, 200, 20, "f32")
     d = np.abs(g - o)
     observed(d, f"shapes-{N}-{B}")
-    assert d.max() <= 2e-3 and np.sqrt(np.mean(d ** 2)) <= 2e-4, (d.max(), np.sqrt(np.mean(d ** 2)))
+    # observed max <= 1.5e-7, rms <= 2.5e-8 (300 steps)
+    assert d.max() <= 2e-6 and np.sqrt(np.mean(d ** 2)) <= 3e-7, (d.max(), np.sqrt(np.mean(d ** 2)))

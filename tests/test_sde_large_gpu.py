@@ -1,8 +1,9 @@
 """N > 96 integrator (wc_sde_large.hip: one GEMM-shaped launch per Euler step)
 vs the CPU oracle, same Philox stream as the N <= 96 path.
 
-Tolerances as tests/test_sde_gpu.py: fp64 max |dE| <= 1e-9; fp32 (bf16x6
-coupling, fp32 state, compensated a_ie) max 2e-3 / rms 2e-4 over short horizons.
+Tolerances: fp64 max |dE| <= 1e-9; fp32 (fp16x3 22-bit coupling, fp32 state,
+compensated a_ie) max 3e-5 / rms 3e-6 over these 120-200-step horizons, about 10x
+the deviation observed on MI355X (max 3.4e-6, rms 2.8e-7).
 Sizes cover BASELINE config 5 (N = 1000 synthetic connectome) and ragged tails
 (B and N not multiples of the 64 x 64 workgroup tile).
 """
@@ -32,7 +33,7 @@ def test_large_vs_oracle(cuda, prec, N, B):
     keys = sim_keys(list(range(B)), [N] * B)
     n = 200 if N < 1000 else 120
     g, o, gb, ob, _ = run_pair(sc, G, S, keys, n // 2, n // 2, n, 7, prec)
-    mx, rms = tol(prec)
+    mx, rms = tol(prec, (3e-5, 3e-6))  # observed f32: max <= 3.4e-6, rms <= 2.8e-7
     d = np.abs(g - o)
     observed(d, f"large-{prec}-{N}-{B}")
     assert d.max() <= mx and np.sqrt(np.mean(d ** 2)) <= rms, (d.max(), np.sqrt(np.mean(d ** 2)))
@@ -84,4 +85,4 @@ def test_large_f32_tracks_f64_statistics(cuda):
         b.integrate(4000, 2.0, 20, rec)
         out[prec] = rec.double().mean(0).cpu().numpy()
     observed(np.abs(out["f32"] - out["f64"]), "large-f32-vs-f64-mean")
-    assert np.abs(out["f32"] - out["f64"]).max() < 0.02
+    assert np.abs(out["f32"] - out["f64"]).max() < 3e-5  # observed 2.7e-6 (6000 steps)

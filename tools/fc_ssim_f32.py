@@ -36,9 +36,17 @@ def main():
     keys = sim_keys([s.seed for s in sims], [s.stream for s in sims])
     sch = Schedule(n_sim=n_sim)
     res, wall = {}, {}
+    last = [time.perf_counter()]
+
+    def progress(phase, step, total):
+        if time.perf_counter() - last[0] > 20:
+            print(f"{prec} {phase} {step}/{total}", flush=True)
+            last[0] = time.perf_counter()
+
     for prec in ("f32", "f64"):
         t = time.perf_counter()
-        res[prec] = run_sweep(sc, G, S, keys, emp, sch, precision=prec, want_fc=True)
+        res[prec] = run_sweep(sc, G, S, keys, emp, sch, precision=prec, want_fc=True, progress=progress,
+                              max_launch_steps=100_000)
         wall[prec] = time.perf_counter() - t
     f32, f64 = res["f32"].fc, res["f64"].fc
     same = np.array([osg.ssim(f32[b], f64[b], 1.0) for b in range(B)])

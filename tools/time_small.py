@@ -36,13 +36,15 @@ def main():
     for v in variants:
         bt = Batch(sc, G[:37], S[:37], keys[:37], p, precision="f32")
         diag(bt, v, 300, 0.05)
-        rec = torch.empty((30, 37, 90), dtype=torch.float32, device="cuda")
+        # diag variants >= 20 record node-major [B*N][ld], ld = records rounded up to 4 (wc_diag_integrate)
+        rec = torch.empty((37 * 90, 32), dtype=torch.float32, device="cuda")
         diag(bt, v, 600, 2.0, 20, rec)
         torch.cuda.synchronize()
-        err[v] = float(np.abs(rec.permute(1, 0, 2).double().cpu().numpy() - orec).max())
+        got = rec[:, :30].reshape(37, 90, 30).permute(0, 2, 1)
+        err[v] = float(np.abs(got.double().cpu().numpy() - orec).max())
     for B in batches:
         bt = Batch(sc, G[:B], S[:B], keys[:B], p, precision="f32")
-        rec = torch.empty((steps // 20, B, 90), dtype=torch.float32, device="cuda")
+        rec = torch.empty((B * 90, (steps // 20 + 3) // 4 * 4), dtype=torch.float32, device="cuda")
         diag(bt, variants[0], 200, 0.05)
         times = {v: [] for v in variants}
         for _ in range(3):
