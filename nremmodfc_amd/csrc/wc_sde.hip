@@ -683,14 +683,17 @@ int launch_f32(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     }
 }
 
+// fp64 parity path: one wave per node tile (NW = NT; E exchanged through LDS), so the
+// latency-bound step of a small batch is spread over NT waves; the per-tile MFMA order is
+// the one-wave kernel's, so the results are the same bits for any NW
 int launch_f64(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     switch (tiles_for(ka.N)) {
         case 1: return launch_v<double, 1, 1, kVarF64>(ka, sc, ws, st);
-        case 2: return launch_v<double, 2, 1, kVarF64>(ka, sc, ws, st);
-        case 3: return launch_v<double, 3, 1, kVarF64>(ka, sc, ws, st);
-        case 4: return launch_v<double, 4, 1, kVarF64>(ka, sc, ws, st);
-        case 5: return launch_v<double, 5, 1, kVarF64>(ka, sc, ws, st);
-        case 6: return launch_v<double, 6, 1, kVarF64>(ka, sc, ws, st);
+        case 2: return launch_v<double, 2, 2, kVarF64>(ka, sc, ws, st);
+        case 3: return launch_v<double, 3, 3, kVarF64>(ka, sc, ws, st);
+        case 4: return launch_v<double, 4, 4, kVarF64>(ka, sc, ws, st);
+        case 5: return launch_v<double, 5, 5, kVarF64>(ka, sc, ws, st);
+        case 6: return launch_v<double, 6, 6, kVarF64>(ka, sc, ws, st);
         default: return wc_set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
     }
 }

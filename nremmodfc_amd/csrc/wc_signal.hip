@@ -60,39 +60,37 @@ struct BoldLayout {
     }
 };
 
-// scipy lfilter (DF2T) in scipy's association order; no fma contraction so the
-// rounding matches the reference path as closely as the hardware allows
-#pragma clang fp contract(off)
+// scipy lfilter (DF2T), one step, with fused multiply-adds (z + x b - y a as two fmas): the
+// oracle (oracle/sigchain.py) keeps scipy's unfused order and is bit-exact with scipy; the
+// device differs from it by rounding only (~1e-16 relative per step; the BOLD tests compare
+// at 1e-7 of max|BOLD| after the whole filtfilt), 6 fp64 operations fewer per sample
 __device__ __forceinline__ double iir_step(double z[4], double x, const double* b, const double* a) {
-    const double y = z[0] + x * b[0];
-    z[0] = z[1] + x * b[1] - y * a[1];
-    z[1] = z[2] + x * b[2] - y * a[2];
-    z[2] = z[3] + x * b[3] - y * a[3];
-    z[3] = x * b[4] - y * a[4];
+    const double y = fma(x, b[0], z[0]);
+    z[0] = fma(x, b[1], fma(-y, a[1], z[1]));
+    z[1] = fma(x, b[2], fma(-y, a[2], z[2]));
+    z[2] = fma(x, b[3], fma(-y, a[3], z[3]));
+    z[3] = fma(x, b[4], -y * a[4]);
     return y;
 }
-// the same step for b[1] == b[3] == 0 (the Bessel band-pass): z + x*0 - y*a == z - y*a
-// exactly for finite x, so the result is bit-identical with two multiplies fewer
+// the same step for b[1] == b[3] == 0 (the Bessel band-pass): fma(x, 0, t) == t exactly
+// for finite x, so the result is bit-identical with two fmas fewer
 __device__ __forceinline__ double iir_step_bp(double z[4], double x, const double* b, const double* a) {
-    const double y = z[0] + x * b[0];
-    z[0] = z[1] - y * a[1];
-    z[1] = z[2] + x * b[2] - y * a[2];
-    z[2] = z[3] - y * a[3];
-    z[3] = x * b[4] - y * a[4];
+    const double y = fma(x, b[0], z[0]);
+    z[0] = fma(-y, a[1], z[1]);
+    z[1] = fma(x, b[2], fma(-y, a[2], z[2]));
+    z[2] = fma(-y, a[3], z[3]);
+    z[3] = fma(x, b[4], -y * a[4]);
     return y;
 }
-#pragma clang fp contract(on)
 
 // e^x for the Balloon's (1 - E0)^(1/f) (|x| < 700): x = k ln2 + r, |r| <= ln2/2,
-// e^r by its degree-13 Taylor polynomial (truncation < 2e-17 relative), 2^k by
+// e^r by its degree-11 Taylor polynomial (truncation < 7e-15 relative), 2^k by
 // ldexp.  Straight-line, no special cases (ocml's exp spends ~20 more instructions
 // on range checks and coefficient moves).
 __device__ __forceinline__ double exp_rr(double x) {
     const double k = __builtin_rint(x * 1.4426950408889634);
     const double r = fma(-k, 1.9082149292705877e-10, fma(-k, 0.6931471803691238, x));  // ln2 hi + lo
-    double p = 1.6059043836821613e-10;                                                 // 1/13!
-    p = fma(p, r, 2.08767569878681e-09);
-    p = fma(p, r, 2.505210838544172e-08);
+    double p = 2.505210838544172e-08;                                                  // 1/11!
     p = fma(p, r, 2.755731922398589e-07);
     p = fma(p, r, 2.7557319223985893e-06);
     p = fma(p, r, 2.48015873015873e-05);
@@ -111,6 +109,7 @@ struct BoldArgs {
     wc_bold_cfg cfg;
     int64_t C, n, M;
     double itaus, itauf, itauo, ialpha, iEo, vo, k1, k2, k3, log1mEo;
+    double bc0, bc1, bc2, bc3;  // BOLD = vo (k1 (1-q) + k2 (1-q/v) + k3 (1-v)) = bc0 - bc1 q - bc2 q/v - bc3 v
     int alpha_3125;  // 1/alpha == 3.125: v^(1/alpha) = v^3 * v^(1/8) by square roots
 };
 
@@ -238,9 +237,9 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? 3 :
             // z = v^(-1/8): fp32 seed (hardware sqrt/rsq), two division-free Newton steps
             // z <- z (1 + (1 - v z^8)/8) (relative error ~1e-16); then 1/v = z^8 and
             // v^(1/alpha) = v^3.125 = v^4 z^7
+            // (one Newton step from the ~3e-7 fp32 seed leaves ~4e-13 relative)
             double z = (double)__builtin_amdgcn_rsqf(__builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf((float)v)));
-#pragma unroll
-            for (int it = 0; it < 2; ++it) {
+            {
                 const double z2 = z * z, z4 = z2 * z2;
                 z = fma(z * 0.125, fma(-v, z4 * z4, 1.0), z);
             }
@@ -253,9 +252,8 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? 3 :
             vpow = exp(log(v) * a.ialpha);
             vpow_iv = vpow * iv;
         }
-        const double bold = a.vo * (a.k1 * (1.0 - q) + a.k2 * (1.0 - q * iv) + a.k3 * (1.0 - v));
-        double rf = (double)__builtin_amdgcn_rcpf((float)f);  // 1/f: fp32 seed + two Newton steps
-        rf = fma(rf, fma(-f, rf, 1.0), rf);
+        const double bold = fma(-a.bc3, v, fma(-a.bc2, q * iv, fma(-a.bc1, q, a.bc0)));
+        double rf = (double)__builtin_amdgcn_rcpf((float)f);  // 1/f: fp32 seed + one Newton step (~1e-14)
         rf = fma(rf, fma(-f, rf, 1.0), rf);
         const double fpow = exp_rr(a.log1mEo * rf);  // (1 - E0)^(1/f)
         const double ds = x - a.itaus * s - a.itauf * (f - 1.0);
@@ -986,6 +984,10 @@ BoldArgs make_bold_args(const wc_bold_cfg* cfg, int64_t C) {
     a.k2 = 2.0;
     a.k3 = 2.0 * Eo - 0.2;
     a.log1mEo = log(1.0 - Eo);
+    a.bc0 = a.vo * (a.k1 + a.k2 + a.k3);
+    a.bc1 = a.vo * a.k1;
+    a.bc2 = a.vo * a.k2;
+    a.bc3 = a.vo * a.k3;
     return a;
 }
 

@@ -250,3 +250,41 @@ def test_sweep_main_n1000_short(tmp_path, cuda):
     assert df[[c for c in sweep.METRIC_COLS if c[:4] in ("ssim", "corr") or c[0] == "e"]].isna().all().all()
     good = df[["sync", "meta", "mean", "peakfreq"]].to_numpy()
     assert np.isfinite(good).all() and (df["peakfreq"] > 0).all()
+
+
+@pytest.mark.gpu
+def test_many_seeds_full_size(tmp_path, cuda):
+    """Config 2 at full size: run_many_seeds.py's 50 seeds x 4 states at the map optima over
+    the full 1001 s schedule (run_many_seeds.py:105-146) -> the collapsed pickle, read the way
+    the figure scripts read it (figures/Fig5/fig5.py:117-129, load(dic, nseeds=50)); the
+    device-batched HMA equals the host facade (the reference's algorithm) on every saved sFC."""
+    import pickle
+    import time
+    from nremmodfc_amd import HMA
+    out = str(tmp_path)
+    t0 = time.perf_counter()
+    sweep.main(["many", "--modality", "map", "--out", out, "--tag", "c2"])
+    print(f"C2 full size: 200 simulations x 1001 s in {time.perf_counter() - t0:.1f} s")
+    with open(os.path.join(out, "c2.pickle"), "rb") as f:  # our own file
+        d = pickle.load(f)
+    assert d["metainfo"] == {s: 50 for s in datasets.STATES}
+    matts = {st: np.zeros((50, 90, 90)) for st in datasets.STATES}
+    hin = {st: np.zeros((50, 90)) for st in datasets.STATES}
+    hse = {st: np.zeros((50, 90)) for st in datasets.STATES}
+    for key in d:
+        if key != "metainfo":
+            s, state = key
+            matts[state][s] = d[key]["sFC"]
+            hin[state][s] = d[key]["Hin_node_sim"]
+            hse[state][s] = d[key]["Hse_node_sim"]
+            assert np.isscalar(d[key]["Hin_sim"]) or np.ndim(d[key]["Hin_sim"]) == 0
+    for st in datasets.STATES:
+        assert np.isfinite(matts[st]).all() and (matts[st] >= 0).all()
+        assert np.isfinite(hin[st]).all() and np.isfinite(hse[st]).all()
+        assert np.allclose(np.diagonal(matts[st], axis1=1, axis2=2), 1.0)
+    for key in [k for k in d if k != "metainfo"]:
+        h = HMA.integration_segregation(d[key]["sFC"].copy())
+        np.testing.assert_allclose(d[key]["Hin_sim"], h["Hin_sim"], rtol=1e-12)
+        np.testing.assert_allclose(d[key]["Hse_sim"], h["Hse_sim"], rtol=1e-11)
+        np.testing.assert_allclose(d[key]["Hin_node_sim"], h["Hin_node_sim"], rtol=1e-9, atol=1e-15)
+        np.testing.assert_allclose(d[key]["Hse_node_sim"], h["Hse_node_sim"], rtol=1e-9, atol=1e-15)

@@ -16,6 +16,7 @@ import sys
 import time
 
 import numpy as np
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -39,6 +40,7 @@ def main():
     last = [time.perf_counter()]
 
     def progress(phase, step, total):
+        torch.cuda.synchronize()  # keep the host in step with the device so the lines reflect finished work
         if time.perf_counter() - last[0] > 20:
             print(f"{prec} {phase} {step}/{total}", flush=True)
             last[0] = time.perf_counter()

@@ -40,6 +40,7 @@ d = {"kernel": kf, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
      "mfma_insts_per_wave_step": vq["SQ_INSTS_MFMA"] / wave_steps,
      "trans_insts_per_wave_step": vq["SQ_INSTS_VALU_TRANS_F32"] / wave_steps,
      "mfma_busy_frac": vq["SQ_VALU_MFMA_BUSY_CYCLES"] / (vq["GRBM_GUI_ACTIVE"] / 8 * simds),
+     "valu_issue_busy_frac": 4 * vq["SQ_ACTIVE_INST_VALU"] / (vq["GRBM_GUI_ACTIVE"] / 8 * simds),
      "note": "rocprofv3 --pmc passes of `python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline` "
              "(tools/profile_bench.sh), averaged per wc_sde_kernel dispatch. FETCH_SIZE x2 (gfx950), KB -> B; "
              "HBM counters include Infinity-Cache traffic. A wave-step = one Euler step of one wave "
@@ -49,7 +50,7 @@ json.dump(d, open("profiles/pmc_sde.json", "w"), indent=1)
 json.dump(d, open("gpurun_out/prof/pmc_sde.json", "w"), indent=1)  # gpurun merges gpurun_out/ back only
 print(json.dumps(d))
 PY
-cp $OUT/bench_kernel_stats.csv profiles/r01_bench_kernel_stats.csv 2>/dev/null || true
+cp $OUT/bench_kernel_stats.csv profiles/r02_bench_kernel_stats.csv 2>/dev/null || true
 # on the GPU box only gpurun_out/ travels back: copy gpurun_out/prof/pmc_sde.json and
 # gpurun_out/prof/bench_kernel_stats.csv into profiles/ afterwards
 tail -1 $OUT/trace.log
