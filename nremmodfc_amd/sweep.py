@@ -338,8 +338,18 @@ def main(argv=None):
 
     if args.kind == "many":
         from . import HMA
+        t0 = time.perf_counter()
         rows, fcs = run_sims(mine, sc, empfcs, sched, args.precision, args.batch, device, want_fc=True)
         hma = HMA.integration_segregation_batch(fcs, device) if fcs else []
+        wall = time.perf_counter() - t0
+        n_steps = len(mine) * sc.shape[0] * sched.n_total
+        perf = json.dumps({"rank": rank, "sims": len(mine), "nodes": sc.shape[0], "wall_s": wall,
+                           "node_steps": n_steps, "node_steps_per_s": n_steps / wall if wall else None,
+                           "includes": "integration, BOLD, FC, metrics, Welch, device HMA",
+                           "batches": getattr(run_sims, "last_timings", None)})
+        print(perf, flush=True)
+        with open(os.path.join(args.out, "temp", f"{tag}_rank{rank}_perf.jsonl"), "a") as f:
+            f.write(perf + "\n")
         save = {(s.seed, s.state): d for s, d in zip(mine, hma)}
         part_path = os.path.join(args.out, "temp", f"{tag}_rank{rank}.pickle")
         with open(part_path + ".tmp", "wb") as f:
