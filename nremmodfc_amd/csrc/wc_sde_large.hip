@@ -29,6 +29,7 @@
 // entry and back at exit.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "wc_common.h"
 #include "wc_device.h"
 
@@ -261,6 +262,39 @@ __device__ __forceinline__ void st_state(T* p, T v) {
     else *p = v;
 }
 
+// wc:80-83 for one (node, simulation) cell on the fp32 product path, with every fusion
+// explicit (contraction off inside): step_kernel and persist_kernel both call this, so the two
+// N > 96 paths give the same bits whatever the surrounding code lets the compiler fuse
+struct CellConsts {
+    float a_ee, a_ei, a_ii, P, rhoE, rE, rI, mu, slI, sqdtD, dtE, dtI, dtA;
+};
+#pragma clang fp contract(off)
+__device__ __forceinline__ void cell_update_f32(const CellConsts& k, float& e, float& in, AccA<true>& A, float cpl,
+                                                float G, float sl, float z, bool pad) {
+    const float e0 = e, in0 = in;
+    const float ai = A.val<float>();
+    float x = k.a_ee * e0;
+    x = __builtin_fmaf(-ai, in0, x);
+    x = __builtin_fmaf(G, cpl, x);
+    x = x + k.P;
+    x = __builtin_fmaf(k.sqdtD, z, x);
+    const float SE = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((k.mu - x) * sl));
+    const float xi = __builtin_fmaf(-k.a_ii, in0, k.a_ei * e0);
+    const float SI = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((k.mu - xi) * k.slI));
+    e = pad ? 0.f : __builtin_fmaf(k.dtE, __builtin_fmaf(__builtin_fmaf(-k.rE, e0, 1.0f), SE, -e0), e0);
+    in = __builtin_fmaf(k.dtI, __builtin_fmaf(__builtin_fmaf(-k.rI, in0, 1.0f), SI, -in0), in0);
+    A.add(k.dtA * (in0 * (e0 - k.rhoE)));
+}
+#pragma clang fp contract(on)
+
+__host__ __device__ inline CellConsts cell_consts(double a_ee, double a_ei, double a_ii, double P, double rhoE,
+                                                  double rE, double rI, double mu, double sigmaI, double sqdtD,
+                                                  double dtSim, double tauE, double tauI, double tau_ip) {
+    return CellConsts{(float)a_ee, (float)a_ei, (float)a_ii, (float)P, (float)rhoE, (float)rE, (float)rI, (float)mu,
+                      (float)(sigmaI * 1.4426950408889634), (float)sqdtD, (float)(dtSim / tauE), (float)(dtSim / tauI),
+                      (float)(dtSim / tau_ip)};
+}
+
 // one Euler step of every simulation; rec_row >= 0: record the state before the update
 // DIAG (ablation, tools/diag_large.py): 1 = no chunk fetch (LDS reused),
 // 2 = no MFMA, 3 = no epilogue state traffic (noise + math only), 4 = nontemporal state
@@ -399,6 +433,8 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
     const Real dt = (Real)a.dtSim, tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;
     const uint64_t gstep = (uint64_t)(a.step0 + s);
     const size_t BN = (size_t)g.B * g.N;
+    const CellConsts kc = cell_consts(a.a_ee, a.a_ei, a.a_ii, a.P, a.rhoE, a.rE, a.rI, a.mu, a.sigmaI, a.sqdtD, a.dtSim,
+                                      a.tauE, a.tauI, a.tau_ip);
     const bool uni = sizeof(Real) == 4 && __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(a.ws + g.o_uni));
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -475,20 +511,21 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             real4 En, In;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const Real e = Ev[r], in = Iv[r];
-                const Real ai = Av[r].template val<Real>();
-                const Real xE = a_ee * e - ai * in + Gv[r] * acc[u][v][r] + P + sqdtD * z[r];
-                const Real SE = Tr<Real>::sig(xE, mu, Sv[r]);
-                const Real SI = Tr<Real>::sig(a_ei * e - a_ii * in, mu, slI);
                 const bool pad = n0 + r >= g.N;  // padding nodes stay exactly 0 (zero B-operand rows)
                 if constexpr (sizeof(Real) == 8) {
+                    const Real e = Ev[r], in = Iv[r];
+                    const Real ai = Av[r].template val<Real>();
+                    const Real xE = a_ee * e - ai * in + Gv[r] * acc[u][v][r] + P + sqdtD * z[r];
+                    const Real SE = Tr<Real>::sig(xE, mu, Sv[r]);
+                    const Real SI = Tr<Real>::sig(a_ei * e - a_ii * in, mu, slI);
                     En[r] = pad ? 0.0 : e + dt * ((-e + (1 - rE * e) * SE) / tauE);
                     In[r] = in + dt * ((-in + (1 - rI * in) * SI) / tauI);
                     Av[r].add(dt * ((in * (e - rhoE)) / tau_ip));
                 } else {
-                    En[r] = pad ? 0.f : e + dtE * (-e + (1 - rE * e) * SE);
-                    In[r] = in + dtI * (-in + (1 - rI * in) * SI);
-                    Av[r].add(dtA * (in * (e - rhoE)));
+                    float e = Ev[r], in = Iv[r];
+                    cell_update_f32(kc, e, in, Av[r], acc[u][v][r], Gv[r], Sv[r], z[r], pad);
+                    En[r] = e;
+                    In[r] = in;
                 }
             }
             if (kState) st_state<kNT>(Iw + t4, In);
@@ -567,10 +604,338 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
     return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
 }
 
+
+// ============================================================================================
+// Persistent fp32 integrator (round 2): the state stays in registers for the whole call.
+//
+// One workgroup (8 waves) owns a tile of 128 nodes x 80 simulations for ALL nsteps steps:
+// wave w holds node tile w (16 nodes) of the five 16-simulation tiles, i.e. 20 (node, sim)
+// cells per lane -- E, I, the a_ie pair, G and the slope in VGPRs.  Each step it streams the
+// connectome rows of its 128 nodes (read-only: LDS-DMA, as in step_kernel) and the whole E
+// image of its 80 simulations, which the 8 node-block workgroups of the simulation block
+// publish every step (every node's E feeds every node's coupling).  The hand-off follows
+// MI355X_MICROARCH.md's validated form (row 1 of its sc1 table): the E image is stored
+// write-through (buffer stores, sc1) and read with sc1 buffer loads only; every storing wave
+// drains vmcnt before a workgroup barrier, after which one lane adds 1 to the simulation
+// block's counter (agent-scope atomic); the consumer's one lane polls that counter with sc1
+// loads, then a workgroup barrier releases the other waves.  One workgroup per CU (the grid
+// never exceeds the CU count and the LDS footprint admits one per CU): every workgroup is
+// resident, so the per-block waits cannot deadlock; every wait is still bounded (a timeout
+// sets the error word and poisons the state with NaN instead of hanging the device).
+// Double-buffered E image: a block writes E(s+1) into the buffer read at step s-1, which
+// every block of its simulation block has finished reading (it passed that block's step-s
+// wait).  The arithmetic per cell -- K order of the MFMA chain, the epilogue expressions,
+// the noise -- is step_kernel's, so both paths give the same bits.
+constexpr int kPN = 128, kPS = 80, kPT = kPS / 16;  // nodes, simulations, simulation tiles per workgroup
+constexpr int kPWaves = kPN / 16;                     // 8
+constexpr uint32_t kSpinLimit = 1u << 22;             // polls per wait before giving up (~seconds)
+
+struct PGeo {
+    int B, N, Np, Bp, MT, NC, SBp, NBp;
+    size_t o_frag, o_scl, o_x, o_cnt, o_err, total;
+};
+
+PGeo pgeometry(int B, int N) {
+    PGeo g{};
+    g.B = B;
+    g.N = N;
+    g.Np = (N + kPN - 1) / kPN * kPN;
+    g.Bp = (B + kPS - 1) / kPS * kPS;
+    g.MT = g.Np / 16;
+    g.NC = g.Np / 32;
+    g.SBp = g.Bp / kPS;
+    g.NBp = g.Np / kPN;
+    size_t o = 0;
+    g.o_frag = o; o += al((size_t)g.MT * g.NC * kParts * 64 * 16);
+    g.o_scl = o; o += al(2 * sizeof(float));
+    g.o_x = o; o += al(2 * (size_t)g.Np * g.Bp * 4);   // two fp16x2 E images
+    g.o_cnt = o; o += al((size_t)g.SBp * 64);           // one counter per simulation block, 64 B apart
+    g.o_err = o; o += al(4);
+    g.total = o;
+    return g;
+}
+
+struct PArgs {
+    double a_ee, a_ei, a_ii, tauE, tauI, P, rhoE, rE, rI, mu, sigmaI, sqdtD, dtSim, tau_ip;
+    const uint64_t* keys;
+    const double* G;
+    const double* sigmaE;
+    double* E;
+    double* I;
+    double* A;
+    void* recE;
+    void* recI;
+    void* recA;
+    int64_t rec_ld, rec_every, step0, nsteps;
+    char* ws;
+    PGeo g;
+};
+
+// E image unit (k-chunk c, simulation block sb, part p, simulation tile t): 64 lanes x 16 B,
+// lane (g, j) holding the 8 fp16 values of nodes 16(2c + h) + 4g + r (jj = 4h + r) of
+// simulation 80 sb + 16 t + j -- the MFMA B-operand fragment, so a chunk of a block is 10
+// contiguous KB
+__host__ __device__ __forceinline__ uint32_t pimg_unit(const PGeo& g, int c, int sb, int p, int t) {
+    return (uint32_t)((((size_t)c * g.SBp + sb) * kParts + p) * kPT + t);
+}
+
+__global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a) {
+    typedef __attribute__((ext_vector_type(4))) float f4;
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    // [stage][node tile x part][lane] A and [stage][part x sim tile][lane] B; each lane's G and
+    // slope (f4 per cell quad) and the 80 simulation keys live in LDS too (registers hold the
+    // state); the 133 KB footprint also admits only one of these workgroups per CU
+    __shared__ f16x8 ldsA[2][kPWaves * kParts][64];
+    __shared__ f16x8 ldsB[2][kParts * kPT][64];
+    __shared__ f4 ldsG[kPT][kPWaves][64];
+    __shared__ f4 ldsS[kPT][kPWaves][64];
+    __shared__ uint64_t ldsK[kPS];
+    __shared__ int go;
+    const PGeo& g = a.g;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, j = lane & 15, gq = lane >> 4;
+    const int sb = blockIdx.x % g.SBp, nb = blockIdx.x / g.SBp;
+    const int mt = nb * kPWaves + w;  // this wave's node tile
+    const int n0 = 16 * mt + 4 * gq;
+    const float* scl = reinterpret_cast<const float*>(a.ws + g.o_scl);
+    const float gscale = scl[1];
+    unsigned* cnt = reinterpret_cast<unsigned*>(a.ws + g.o_cnt) + sb * 16;
+    unsigned* err = reinterpret_cast<unsigned*>(a.ws + g.o_err);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(a.ws + g.o_x, 0,
+                                                                         (int)(2 * (size_t)g.Np * g.Bp * 4), 0x00020000);
+    const uint32_t img_units = (uint32_t)((size_t)g.Np * g.Bp * 4 / 1024);  // 1-KB units (64 lanes x 16 B) per image
+
+    // ---- state into registers, parameters into LDS (step_kernel's prep_kernel arithmetic) ----
+    float E[kPT][4], I[kPT][4];
+    AccA<true> Av[kPT][4];
+    if (tid < kPS) {
+        const int b = sb * kPS + tid;
+        ldsK[tid] = a.keys[b < g.B ? b : g.B - 1];
+    }
+#pragma unroll
+    for (int t = 0; t < kPT; ++t) {
+        const int b = sb * kPS + 16 * t + j;
+        f4 gv, sv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = n0 + r;
+            const bool ok = b < g.B && n < g.N;
+            const size_t o = ok ? (size_t)b * g.N + n : 0;
+            E[t][r] = ok ? (float)a.E[o] : 0.f;
+            I[t][r] = ok ? (float)a.I[o] : 0.f;
+            Av[t][r].set(ok ? a.A[o] : 0.0);
+            gv[r] = ok ? (float)a.G[o] * gscale : 0.f;
+            sv[r] = ok ? Tr<float>::slope(a.sigmaE[o]) : 0.f;
+        }
+        ldsG[t][w][lane] = gv;
+        ldsS[t][w][lane] = sv;
+    }
+    // publish this wave's E tiles into image `buf` (write-through stores)
+    auto publish = [&](int buf) {
+#pragma unroll
+        for (int t = 0; t < kPT; ++t) {
+            f16x4 ph[kParts];
+            split2h(E[t], ph[0], ph[1]);
+#pragma unroll
+            for (int p = 0; p < kParts; ++p) {
+                const uint32_t unit = buf * img_units + pimg_unit(g, mt >> 1, sb, p, t);
+                const int off = (int)((unit * 64 + lane) * 16 + (mt & 1) * 8);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, ph[p]), xrs, off, 0, 16);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the barrier
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // wait until every node block of this simulation block has published `target` images
+    auto wait_for = [&](unsigned target) -> bool {
+        if (tid == 0) {
+            int ok = 0;
+            for (uint32_t it = 0; it < kSpinLimit; ++it) {
+                if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+                    ok = 1;
+                    break;
+                }
+                if ((it & 63) == 63 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!ok) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            go = ok;
+        }
+        __syncthreads();
+        return go != 0;
+    };
+
+    publish(0);
+    bool alive = wait_for((unsigned)g.NBp);
+    const f16x8* F = reinterpret_cast<const f16x8*>(a.ws + g.o_frag);
+    const CellConsts kc = cell_consts(a.a_ee, a.a_ei, a.a_ii, a.P, a.rhoE, a.rE, a.rI, a.mu, a.sigmaI, a.sqdtD, a.dtSim,
+                                      a.tauE, a.tauI, a.tau_ip);
+    const size_t BN = (size_t)g.B * g.N;
+    int rec_cnt = 0, rec_row = 0;
+    // this wave's share of a chunk: A units 2w, 2w+1 (node tile w, parts 0/1) by LDS-DMA;
+    // B: 640 16-B units of the chunk, thread tid takes unit-lane tid and (tid < 128) 512 + tid
+    const f16x8* asrc0 = F + ((size_t)mt * g.NC * kParts + 0) * 64 + lane;
+    const f16x8* asrc1 = F + ((size_t)mt * g.NC * kParts + 1) * 64 + lane;
+    u4 rb0, rb1;
+    auto issue = [&](int c, int st, int buf) {
+        __builtin_amdgcn_global_load_lds(asrc0 + (size_t)c * kParts * 64, (lds_vptr)(&ldsA[st][2 * w][lane]), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(asrc1 + (size_t)c * kParts * 64, (lds_vptr)(&ldsA[st][2 * w + 1][lane]), 16, 0, 0);
+        const uint32_t base = (buf * img_units + pimg_unit(g, c, sb, 0, 0)) * 64;  // chunk's 640 units
+        rb0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)((base + tid) * 16), 0, 16);
+        if (tid < 128) rb1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)((base + 512 + tid) * 16), 0, 16);
+    };
+    for (int64_t s = 0; s < a.nsteps && alive; ++s) {
+        const int buf = (int)(s & 1);
+        const bool rec = a.rec_every > 0 && rec_cnt == 0;
+        if (a.rec_every > 0) {
+            if (rec_cnt == 0) rec_cnt = (int)a.rec_every;
+            --rec_cnt;
+        }
+        f4 acc[kPT];
+#pragma unroll
+        for (int t = 0; t < kPT; ++t) acc[t] = f4{0, 0, 0, 0};
+        issue(0, 0, buf);
+        for (int c = 0; c < g.NC; ++c) {
+            const int st = c & 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c: A in LDS, B in registers
+            reinterpret_cast<u4*>(&ldsB[st][0][0])[tid] = rb0;
+            if (tid < 128) reinterpret_cast<u4*>(&ldsB[st][0][0])[512 + tid] = rb1;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (c + 1 < g.NC) issue(c + 1, st ^ 1, buf);  // stage st^1 was last read at chunk c-1
+            const f16x8 fa0 = ldsA[st][2 * w][lane], fa1 = ldsA[st][2 * w + 1][lane];
+#pragma unroll
+            for (int t = 0; t < kPT; ++t) {
+                const f16x8 fb0 = ldsB[st][t][lane], fb1 = ldsB[st][kPT + t][lane];
+                // small terms first (2^-11: lo.hi, hi.lo; 1: hi.hi), as in step_kernel
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa1, fb0, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa0, fb1, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa0, fb0, acc[t], 0, 0, 0);
+            }
+        }
+        // ---- epilogue: step_kernel's update on the D fragments (the state in registers) ----
+        const uint64_t gstep = (uint64_t)(a.step0 + s);
+#pragma unroll
+        for (int t = 0; t < kPT; ++t) {
+            __builtin_amdgcn_sched_barrier(0);  // one simulation tile at a time: bounded live ranges
+            const int b = sb * kPS + 16 * t + j;
+            const bool live = b < g.B;
+            if (rec && live) {
+                // record offsets recomputed per record (opaque N, ld): hoisted out of the step loop
+                // they would pin 40 VGPRs of 64-bit addresses for the whole launch
+                int Nn = g.N;
+                int64_t ld = a.rec_ld;
+                asm volatile("" : "+s"(Nn), "+s"(ld));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = n0 + r;
+                    if (n < Nn) {
+                        const size_t cc = (size_t)b * Nn + n;
+                        const size_t o = ld ? cc * ld + rec_row : (size_t)rec_row * BN + cc;
+                        static_cast<float*>(a.recE)[o] = E[t][r];
+                        if (a.recI) static_cast<float*>(a.recI)[o] = I[t][r];
+                        if (a.recA) static_cast<float*>(a.recA)[o] = (float)Av[t][r].get();
+                    }
+                }
+            }
+            float z[4];
+            quad_normals(gstep, (uint32_t)(4 * mt + gq), ldsK[16 * t + j], z);
+            const f4 gv = ldsG[t][w][lane], sv = ldsS[t][w][lane];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                cell_update_f32(kc, E[t][r], I[t][r], Av[t][r], acc[t][r], gv[r], sv[r], z[r], n0 + r >= g.N);
+        }
+        if (rec) ++rec_row;
+        if (s + 1 < a.nsteps) {
+            publish(buf ^ 1);
+            alive = wait_for((unsigned)g.NBp * (unsigned)(s + 2));
+        }
+    }
+    // ---- state back to the caller's fp64 arrays (NaN if a wait timed out) ----
+    const bool poisoned = !alive;
+#pragma unroll
+    for (int t = 0; t < kPT; ++t) {
+        const int b = sb * kPS + 16 * t + j;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int n = n0 + r;
+            if (b < g.B && n < g.N) {
+                const size_t o = (size_t)b * g.N + n;
+                a.E[o] = poisoned ? __builtin_nan("") : (double)E[t][r];
+                a.I[o] = (double)I[t][r];
+                a.A[o] = Av[t][r].get();
+            }
+        }
+    }
+}
+
+int cu_count_large() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return n;
+}
+
+// OPT-IN (WCSDE_PERSISTENT=1): measured on MI355X it is no faster than step_kernel -- 33.7 vs
+// 32.8 us per step in the C5 bench pipeline (35.9 vs 38.0 with node-major ring records), and
+// 33.3 us at half the batch: the K loop waits 32 times per step on MALL-latency sc1 loads of the
+// freshly published E image, which the register budget (state + 20 accumulators at 2 waves per
+// SIMD) does not let it prefetch deeper.  It applies when every workgroup gets a
+// CU of its own (residency) and the image offsets fit the 32-bit buffer descriptors.
+bool persistent_ok(int B, int N) {
+    const char* env = getenv("WCSDE_PERSISTENT");
+    if (!env || env[0] != '1') return false;
+    const PGeo g = pgeometry(B, N);
+    if (2 * (size_t)g.Np * g.Bp * 4 >= (size_t)INT32_MAX) return false;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)persist_kernel, kPWaves * 64, 0) != hipSuccess ||
+        occ < 1)
+        return false;
+    return g.SBp * g.NBp <= cu_count_large();
+}
+
+int run_persistent(const wc_params* p, int B, int N, const double* sc, const double* G, const double* sigmaE,
+                   const uint64_t* keys, double* E, double* I, double* A, int64_t step0, int64_t nsteps,
+                   double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI, void* recA,
+                   void* workspace, hipStream_t st) {
+    PArgs a{};
+    a.a_ee = p->a_ee; a.a_ei = p->a_ei; a.a_ii = p->a_ii; a.tauE = p->tauE; a.tauI = p->tauI;
+    a.P = p->P; a.rhoE = p->rhoE; a.rE = p->rE; a.rI = p->rI; a.mu = p->mu; a.sigmaI = p->sigmaI;
+    a.sqdtD = p->sqdtD; a.dtSim = p->dtSim; a.tau_ip = tau_ip;
+    a.keys = keys; a.G = G; a.sigmaE = sigmaE; a.E = E; a.I = I; a.A = A;
+    a.recE = recE; a.recI = recI; a.recA = recA; a.rec_ld = rec_ld; a.rec_every = rec_every;
+    a.step0 = step0; a.nsteps = nsteps;
+    a.ws = static_cast<char*>(workspace);
+    a.g = pgeometry(B, N);
+    const PGeo& g = a.g;
+    // connectome image in the 128-node padding (frag_f16_kernel takes a Geo)
+    Geo fg{};
+    fg.N = N;
+    fg.Np = g.Np;
+    fg.MT = g.MT;
+    fg.NC = g.NC;
+    float* scl = reinterpret_cast<float*>(a.ws + g.o_scl);
+    hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(1024), 0, st, sc, N, scl);
+    const int n = g.MT * g.NC * 64;
+    hipLaunchKernelGGL(frag_f16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc, fg, scl,
+                       reinterpret_cast<f16x8*>(a.ws + g.o_frag));
+    hipError_t me = hipMemsetAsync(a.ws + g.o_cnt, 0, g.o_err + al(4) - g.o_cnt, st);  // counters + error word
+    if (me != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(me));
+    hipLaunchKernelGGL(persist_kernel, dim3((unsigned)(g.SBp * g.NBp)), dim3(kPWaves * 64), 0, st, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
+}
+
 }  // namespace
 
 // internal entry points used by wc_sde.hip's dispatcher
-size_t wc_large_workspace_size(int B, int N, int precision) { return geometry(B, N, precision).total; }
+size_t wc_large_workspace_size(int B, int N, int precision) {
+    const size_t st = geometry(B, N, precision).total;
+    if (precision != WC_F32) return st;
+    const size_t pe = pgeometry(B, N).total;  // the persistent path's layout (same workspace, reused)
+    return st > pe ? st : pe;
+}
 
 int wc_large_integrate(const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
                        const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
@@ -579,6 +944,9 @@ int wc_large_integrate(const wc_params* p, int precision, int B, int N, const do
     if (precision == WC_F64)
         return run_large<double>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld,
                                  recE, recI, recA, workspace, st);
+    if (nsteps > 1 && persistent_ok(B, N))
+        return run_persistent(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld, recE,
+                              recI, recA, workspace, st);
     return run_large<float>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld, recE,
                             recI, recA, workspace, st);
 }

@@ -86,3 +86,67 @@ def test_large_f32_tracks_f64_statistics(cuda):
         out[prec] = rec.double().mean(0).cpu().numpy()
     observed(np.abs(out["f32"] - out["f64"]), "large-f32-vs-f64-mean")
     assert np.abs(out["f32"] - out["f64"]).max() < 3e-5  # observed 2.7e-6 (6000 steps)
+
+
+def _both_paths(sc, G, S, keys, steps, rec_every=20, rec_ld=0, chunks=None):
+    """The same integration through the persistent kernel (opt-in, WCSDE_PERSISTENT=1) and through
+    the one-launch-per-step product kernel: final state and records."""
+    import os
+    out = {}
+    for flag in ("1", "0"):
+        os.environ["WCSDE_PERSISTENT"] = flag
+        try:
+            b = Batch(sc, G, S, keys, precision="f32")
+            b.integrate(60, 0.05)
+            n_rec = -(-steps // rec_every)
+            if rec_ld:
+                rec = torch.zeros((b.B * b.N * rec_ld,), dtype=torch.float32, device="cuda")
+                b.integrate(steps, 2.0, rec_every, rec, rec_ld=rec_ld)
+            else:
+                rec = torch.empty((n_rec, b.B, b.N), dtype=torch.float32, device="cuda")
+                done = 0
+                for n in (chunks or [steps]):
+                    b.integrate(n, 2.0, rec_every, rec[done // rec_every:])
+                    done += n
+            torch.cuda.synchronize()
+            out[flag] = (b.E.clone(), b.I.clone(), b.A.clone(), rec)
+        finally:
+            os.environ.pop("WCSDE_PERSISTENT", None)
+    return out["1"], out["0"]
+
+
+@pytest.mark.parametrize("N,B", [(1000, 2500), (250, 170), (97, 1)])
+def test_persistent_matches_step_kernel(cuda, N, B):
+    """Round 2's persistent kernel (state in registers, in-launch E-image hand-off between the
+    node-block workgroups of a simulation block) gives the step kernel's bits: same MFMA order,
+    same epilogue arithmetic.  C5 shard, ragged tiles (3 x 2 workgroups), a single simulation."""
+    sc = _sc(N, 21)
+    rng = np.random.default_rng(N)
+    G = 0.16 + rng.uniform(-0.1, 0.3, B)
+    S = 7.68 + rng.uniform(-0.2, 0.2, B)
+    keys = sim_keys(np.arange(B) % 50, np.arange(B) // 50 + 7)
+    p, s = _both_paths(sc, G, S, keys, 300)
+    for name, x, y in zip(("E", "I", "A", "rec"), p, s):
+        d = (x.double() - y.double()).abs()
+        if not torch.equal(x, y):
+            first = int(torch.nonzero(d.reshape(d.shape[0], -1).amax(1) if name == "rec" else d.reshape(-1))[0, 0])
+            print(f"{name}: max |d| {d.max().item():.3e}, {int((d > 0).sum())} of {d.numel()} differ, first {first}")
+    for x, y in zip(p, s):
+        assert torch.equal(x, y)
+    assert torch.isfinite(p[0]).all()
+
+
+def test_persistent_maps_ring_and_chunks(cuda):
+    """Per-node G and sigma (maps mode), node-major ring records, and chunked calls."""
+    N, B = 1000, 90
+    sc = _sc(N, 5)
+    m = datasets.synthetic_map(N)
+    G = np.stack([0.16 + d * m for d in np.linspace(-0.1, 0.28, B)])
+    S = np.stack([7.68 + d * m[::-1] for d in np.linspace(-0.2, 0.18, B)])
+    keys = sim_keys([3] * B, list(range(B)))
+    p, s = _both_paths(sc, G, S, keys, 200, rec_every=20, rec_ld=12)
+    for x, y in zip(p, s):
+        assert torch.equal(x, y)
+    p, s = _both_paths(sc, G, S, keys, 200, rec_every=20, chunks=[40, 100, 60])
+    for x, y in zip(p, s):
+        assert torch.equal(x, y)
