@@ -262,37 +262,39 @@ __device__ __forceinline__ void st_state(T* p, T v) {
     else *p = v;
 }
 
-// wc:80-83 for one (node, simulation) cell on the fp32 product path, with every fusion
-// explicit (contraction off inside): step_kernel and persist_kernel both call this, so the two
-// N > 96 paths give the same bits whatever the surrounding code lets the compiler fuse
+// wc:80-83 for one (node, simulation) cell on the fp32 product path: the folded-constant form of
+// wc_sde.hip's fast path (x' = xE - mu, log2-based sigmoids, the noise scale with sqrt(2 ln 2)
+// folded in for the raw Box-Muller normal, a_ie read as its high word), with every fusion
+// explicit (contraction off inside).  step_kernel and persist_kernel both call this, so the two
+// N > 96 paths give the same bits whatever the surrounding code lets the compiler fuse.
 struct CellConsts {
-    float a_ee, a_ei, a_ii, P, rhoE, rE, rI, mu, slI, sqdtD, dtE, dtI, dtA;
+    float a_ee, Pm, rhoE, rE, rI, cIe, cIi, cI0, knoise, dtE, dtI, dtA;
 };
 #pragma clang fp contract(off)
 __device__ __forceinline__ void cell_update_f32(const CellConsts& k, float& e, float& in, AccA<true>& A, float cpl,
-                                                float G, float sl, float z, bool pad) {
+                                                float G, float sl, float zraw, bool pad) {
     const float e0 = e, in0 = in;
-    const float ai = A.val<float>();
-    float x = k.a_ee * e0;
+    const float ai = A.fast();
+    float x = __builtin_fmaf(k.a_ee, e0, k.Pm);
     x = __builtin_fmaf(-ai, in0, x);
     x = __builtin_fmaf(G, cpl, x);
-    x = x + k.P;
-    x = __builtin_fmaf(k.sqdtD, z, x);
-    const float SE = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((k.mu - x) * sl));
-    const float xi = __builtin_fmaf(-k.a_ii, in0, k.a_ei * e0);
-    const float SI = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((k.mu - xi) * k.slI));
+    x = __builtin_fmaf(k.knoise, zraw, x);
+    const float SE = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-(x * sl)));
+    const float SI = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(e0, k.cIe, __builtin_fmaf(in0, k.cIi, k.cI0))));
     e = pad ? 0.f : __builtin_fmaf(k.dtE, __builtin_fmaf(__builtin_fmaf(-k.rE, e0, 1.0f), SE, -e0), e0);
     in = __builtin_fmaf(k.dtI, __builtin_fmaf(__builtin_fmaf(-k.rI, in0, 1.0f), SI, -in0), in0);
-    A.add(k.dtA * (in0 * (e0 - k.rhoE)));
+    const float tA = in0 * k.dtA;
+    A.add(__builtin_fmaf(e0, tA, -k.rhoE * tA));
 }
 #pragma clang fp contract(on)
 
 __host__ __device__ inline CellConsts cell_consts(double a_ee, double a_ei, double a_ii, double P, double rhoE,
                                                   double rE, double rI, double mu, double sigmaI, double sqdtD,
                                                   double dtSim, double tauE, double tauI, double tau_ip) {
-    return CellConsts{(float)a_ee, (float)a_ei, (float)a_ii, (float)P, (float)rhoE, (float)rE, (float)rI, (float)mu,
-                      (float)(sigmaI * 1.4426950408889634), (float)sqdtD, (float)(dtSim / tauE), (float)(dtSim / tauI),
-                      (float)(dtSim / tau_ip)};
+    const double l2e = 1.4426950408889634;
+    return CellConsts{(float)a_ee, (float)(P - mu), (float)rhoE, (float)rE, (float)rI, (float)(-a_ei * sigmaI * l2e),
+                      (float)(a_ii * sigmaI * l2e), (float)(mu * sigmaI * l2e), (float)(sqdtD * (double)kSqrt2Ln2),
+                      (float)(dtSim / tauE), (float)(dtSim / tauI), (float)(dtSim / tau_ip)};
 }
 
 // one Euler step of every simulation; rec_row >= 0: record the state before the update
@@ -507,7 +509,8 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
                 }
             }
             Real z[4];
-            quad_normals(gstep, (uint32_t)(4 * mt + gq), key, z);
+            if constexpr (sizeof(Real) == 4) quad_normals_raw(gstep, (uint32_t)(4 * mt + gq), key, z);
+            else quad_normals(gstep, (uint32_t)(4 * mt + gq), key, z);
             real4 En, In;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -656,7 +659,7 @@ PGeo pgeometry(int B, int N) {
 }
 
 struct PArgs {
-    double a_ee, a_ei, a_ii, tauE, tauI, P, rhoE, rE, rI, mu, sigmaI, sqdtD, dtSim, tau_ip;
+    CellConsts kc;  // folded on the host (cell_consts): no fp64 constant math inside the step loop
     const uint64_t* keys;
     const double* G;
     const double* sigmaE;
@@ -681,17 +684,13 @@ __host__ __device__ __forceinline__ uint32_t pimg_unit(const PGeo& g, int c, int
 
 __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a) {
     typedef __attribute__((ext_vector_type(4))) float f4;
-    typedef unsigned u4 __attribute__((ext_vector_type(4)));
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    // [stage][node tile x part][lane] A and [stage][part x sim tile][lane] B; each lane's G and
-    // slope (f4 per cell quad) and the 80 simulation keys live in LDS too (registers hold the
-    // state); the 133 KB footprint also admits only one of these workgroups per CU
-    __shared__ f16x8 ldsA[2][kPWaves * kParts][64];
+    // [stage][part x sim tile][lane] B (2 stages); per-simulation G, slope and keys.  The state and
+    // the A fragments live in registers (~215 VGPRs: one workgroup per CU).
     __shared__ f16x8 ldsB[2][kParts * kPT][64];
-    __shared__ f4 ldsG[kPT][kPWaves][64];
-    __shared__ f4 ldsS[kPT][kPWaves][64];
+    __shared__ float2 ldsGS[kPS];
     __shared__ uint64_t ldsK[kPS];
-    __shared__ int go;
+    __shared__ int go, uni;
     const PGeo& g = a.g;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, j = lane & 15, gq = lane >> 4;
     const int sb = blockIdx.x % g.SBp, nb = blockIdx.x / g.SBp;
@@ -704,18 +703,26 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(a.ws + g.o_x, 0,
                                                                          (int)(2 * (size_t)g.Np * g.Bp * 4), 0x00020000);
     const uint32_t img_units = (uint32_t)((size_t)g.Np * g.Bp * 4 / 1024);  // 1-KB units (64 lanes x 16 B) per image
+    const f16x8* X = reinterpret_cast<const f16x8*>(a.ws + g.o_x);
 
-    // ---- state into registers, parameters into LDS (step_kernel's prep_kernel arithmetic) ----
-    float E[kPT][4], I[kPT][4];
-    AccA<true> Av[kPT][4];
+    // ---- state into registers (step_kernel's prep_kernel arithmetic); G and slope per
+    // simulation when this workgroup's cells do not vary by node (every sweep but the maps
+    // modes), else read per cell at each step ----
+    if (tid == 0) uni = 1;
     if (tid < kPS) {
         const int b = sb * kPS + tid;
-        ldsK[tid] = a.keys[b < g.B ? b : g.B - 1];
+        const int bb = b < g.B ? b : g.B - 1;
+        ldsK[tid] = a.keys[bb];
+        ldsGS[tid] = b < g.B ? make_float2((float)a.G[(size_t)bb * g.N] * gscale, Tr<float>::slope(a.sigmaE[(size_t)bb * g.N]))
+                             : make_float2(0.f, 0.f);
     }
+    __syncthreads();
+    float E[kPT][4], I[kPT][4];
+    AccA<true> Av[kPT][4];
+    bool my_uni = true;
 #pragma unroll
     for (int t = 0; t < kPT; ++t) {
         const int b = sb * kPS + 16 * t + j;
-        f4 gv, sv;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int n = n0 + r;
@@ -724,13 +731,13 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             E[t][r] = ok ? (float)a.E[o] : 0.f;
             I[t][r] = ok ? (float)a.I[o] : 0.f;
             Av[t][r].set(ok ? a.A[o] : 0.0);
-            gv[r] = ok ? (float)a.G[o] * gscale : 0.f;
-            sv[r] = ok ? Tr<float>::slope(a.sigmaE[o]) : 0.f;
+            if (ok && (a.G[o] != a.G[(size_t)b * g.N] || a.sigmaE[o] != a.sigmaE[(size_t)b * g.N])) my_uni = false;
         }
-        ldsG[t][w][lane] = gv;
-        ldsS[t][w][lane] = sv;
     }
-    // publish this wave's E tiles into image `buf` (write-through stores)
+    if (!my_uni) uni = 0;  // benign race: every writer stores 0
+    // publish this wave's E tiles into image `buf` and release them to the simulation block:
+    // write-through stores, a vmcnt drain in every storing wave, a workgroup barrier, one lane's
+    // agent-scope release and counter add (MI355X_MICROARCH.md "Valid forms", producer)
     auto publish = [&](int buf) {
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
@@ -743,11 +750,16 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, ph[p]), xrs, off, 0, 16);
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     };
-    // wait until every node block of this simulation block has published `target` images
+    // consumer: one lane polls the counter (relaxed, sc1 loads), then ONE agent acquire, a vmcnt
+    // wait and a workgroup barrier before any wave loads the image (bounded: error word + exit)
     auto wait_for = [&](unsigned target) -> bool {
         if (tid == 0) {
             int ok = 0;
@@ -760,6 +772,8 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
                 __builtin_amdgcn_s_sleep(1);
             }
             if (!ok) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             go = ok;
         }
         __syncthreads();
@@ -768,22 +782,46 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
 
     publish(0);
     bool alive = wait_for((unsigned)g.NBp);
+    const bool uni_wg = uni != 0;  // (the barriers inside publish/wait_for ordered every store to it)
     const f16x8* F = reinterpret_cast<const f16x8*>(a.ws + g.o_frag);
-    const CellConsts kc = cell_consts(a.a_ee, a.a_ei, a.a_ii, a.P, a.rhoE, a.rE, a.rI, a.mu, a.sigmaI, a.sqdtD, a.dtSim,
-                                      a.tauE, a.tauI, a.tau_ip);
+    CellConsts kc = a.kc;
+    // the folded constants stay in VGPRs (wave-uniform values; as SGPRs they were spilled to VGPR
+    // lanes and re-read every step)
+    asm volatile("" : "+v"(kc.a_ee), "+v"(kc.Pm), "+v"(kc.rhoE), "+v"(kc.rE), "+v"(kc.rI), "+v"(kc.cIe));
+    asm volatile("" : "+v"(kc.cIi), "+v"(kc.cI0), "+v"(kc.knoise), "+v"(kc.dtE), "+v"(kc.dtI), "+v"(kc.dtA));
     const size_t BN = (size_t)g.B * g.N;
     int rec_cnt = 0, rec_row = 0;
-    // this wave's share of a chunk: A units 2w, 2w+1 (node tile w, parts 0/1) by LDS-DMA;
-    // B: 640 16-B units of the chunk, thread tid takes unit-lane tid and (tid < 128) 512 + tid
-    const f16x8* asrc0 = F + ((size_t)mt * g.NC * kParts + 0) * 64 + lane;
-    const f16x8* asrc1 = F + ((size_t)mt * g.NC * kParts + 1) * 64 + lane;
-    u4 rb0, rb1;
-    auto issue = [&](int c, int st, int buf) {
-        __builtin_amdgcn_global_load_lds(asrc0 + (size_t)c * kParts * 64, (lds_vptr)(&ldsA[st][2 * w][lane]), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(asrc1 + (size_t)c * kParts * 64, (lds_vptr)(&ldsA[st][2 * w + 1][lane]), 16, 0, 0);
-        const uint32_t base = (buf * img_units + pimg_unit(g, c, sb, 0, 0)) * 64;  // chunk's 640 units
-        rb0 = __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)((base + tid) * 16), 0, 16);
-        if (tid < 128) rb1 = __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)((base + 512 + tid) * 16), 0, 16);
+    // K loop operands, two chunks ahead, through registers: A = this wave's own node tile (units
+    // 2w, 2w+1 of the read-only connectome image) straight into MFMA fragments; B = the chunk's
+    // 640 E-image units, thread tid loading unit-lane tid (and 512 + tid for tid < 128), written
+    // to one of two LDS stages once they land
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const f16x8* asrc = F + (size_t)mt * g.NC * kParts * 64 + lane;
+    const u4* X4 = reinterpret_cast<const u4*>(X);
+    f16x8 fa[2][kParts];
+    u4 rb[2][2];
+    auto load_chunk = [&](int c, int slot, int buf) {
+        const f16x8* ap = asrc + (size_t)c * kParts * 64;
+        fa[slot][0] = ap[0];
+        fa[slot][1] = ap[64];
+        const u4* xb = X4 + (size_t)(buf * img_units + pimg_unit(g, c, sb, 0, 0)) * 64;
+        rb[slot][0] = xb[tid];
+        if (tid < 128) rb[slot][1] = xb[512 + tid];
+    };
+    auto do_chunk = [&](int c, int slot, int buf, f4 (&acc)[kPT]) {
+        reinterpret_cast<u4*>(&ldsB[slot][0][0])[tid] = rb[slot][0];
+        if (tid < 128) reinterpret_cast<u4*>(&ldsB[slot][0][0])[512 + tid] = rb[slot][1];
+        __syncthreads();  // stage `slot` was last read at chunk c - 2, before the previous barrier
+        const f16x8 a0 = fa[slot][0], a1 = fa[slot][1];
+        if (c + 2 < g.NC) load_chunk(c + 2, slot, buf);
+#pragma unroll
+        for (int t = 0; t < kPT; ++t) {
+            const f16x8 fb0 = ldsB[slot][t][lane], fb1 = ldsB[slot][kPT + t][lane];
+            // small terms first (2^-11: lo.hi, hi.lo; 1: hi.hi), as in step_kernel
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, fb0, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb1, acc[t], 0, 0, 0);
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb0, acc[t], 0, 0, 0);
+        }
     };
     for (int64_t s = 0; s < a.nsteps && alive; ++s) {
         const int buf = (int)(s & 1);
@@ -795,24 +833,11 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         f4 acc[kPT];
 #pragma unroll
         for (int t = 0; t < kPT; ++t) acc[t] = f4{0, 0, 0, 0};
-        issue(0, 0, buf);
-        for (int c = 0; c < g.NC; ++c) {
-            const int st = c & 1;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c: A in LDS, B in registers
-            reinterpret_cast<u4*>(&ldsB[st][0][0])[tid] = rb0;
-            if (tid < 128) reinterpret_cast<u4*>(&ldsB[st][0][0])[512 + tid] = rb1;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            if (c + 1 < g.NC) issue(c + 1, st ^ 1, buf);  // stage st^1 was last read at chunk c-1
-            const f16x8 fa0 = ldsA[st][2 * w][lane], fa1 = ldsA[st][2 * w + 1][lane];
-#pragma unroll
-            for (int t = 0; t < kPT; ++t) {
-                const f16x8 fb0 = ldsB[st][t][lane], fb1 = ldsB[st][kPT + t][lane];
-                // small terms first (2^-11: lo.hi, hi.lo; 1: hi.hi), as in step_kernel
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa1, fb0, acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa0, fb1, acc[t], 0, 0, 0);
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa0, fb0, acc[t], 0, 0, 0);
-            }
+        load_chunk(0, 0, buf);
+        load_chunk(1, 1, buf);
+        for (int c = 0; c < g.NC; c += 2) {  // NC is a multiple of 4 (nodes padded to 128)
+            do_chunk(c, 0, buf, acc);
+            do_chunk(c + 1, 1, buf, acc);
         }
         // ---- epilogue: step_kernel's update on the D fragments (the state in registers) ----
         const uint64_t gstep = (uint64_t)(a.step0 + s);
@@ -821,12 +846,12 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             __builtin_amdgcn_sched_barrier(0);  // one simulation tile at a time: bounded live ranges
             const int b = sb * kPS + 16 * t + j;
             const bool live = b < g.B;
+            // record offsets and per-cell parameter addresses recomputed here (opaque N, ld):
+            // hoisted out of the step loop they would pin dozens of VGPRs of 64-bit addresses
+            int Nn = g.N;
+            int64_t ld = a.rec_ld;
+            asm volatile("" : "+s"(Nn), "+s"(ld));
             if (rec && live) {
-                // record offsets recomputed per record (opaque N, ld): hoisted out of the step loop
-                // they would pin 40 VGPRs of 64-bit addresses for the whole launch
-                int Nn = g.N;
-                int64_t ld = a.rec_ld;
-                asm volatile("" : "+s"(Nn), "+s"(ld));
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int n = n0 + r;
@@ -840,8 +865,25 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
                 }
             }
             float z[4];
-            quad_normals(gstep, (uint32_t)(4 * mt + gq), ldsK[16 * t + j], z);
-            const f4 gv = ldsG[t][w][lane], sv = ldsS[t][w][lane];
+            quad_normals_raw(gstep, (uint32_t)(4 * mt + gq), ldsK[16 * t + j], z);
+            float gv[4], sv[4];
+            if (uni_wg) {
+                const float2 gs = ldsGS[16 * t + j];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    gv[r] = gs.x;
+                    sv[r] = gs.y;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int n = n0 + r;
+                    const bool ok = live && n < Nn;
+                    const size_t o = ok ? (size_t)b * Nn + n : 0;
+                    gv[r] = ok ? (float)a.G[o] * gscale : 0.f;
+                    sv[r] = ok ? Tr<float>::slope(a.sigmaE[o]) : 0.f;
+                }
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r)
                 cell_update_f32(kc, E[t][r], I[t][r], Av[t][r], acc[t][r], gv[r], sv[r], z[r], n0 + r >= g.N);
@@ -900,9 +942,8 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
                    double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI, void* recA,
                    void* workspace, hipStream_t st) {
     PArgs a{};
-    a.a_ee = p->a_ee; a.a_ei = p->a_ei; a.a_ii = p->a_ii; a.tauE = p->tauE; a.tauI = p->tauI;
-    a.P = p->P; a.rhoE = p->rhoE; a.rE = p->rE; a.rI = p->rI; a.mu = p->mu; a.sigmaI = p->sigmaI;
-    a.sqdtD = p->sqdtD; a.dtSim = p->dtSim; a.tau_ip = tau_ip;
+    a.kc = cell_consts(p->a_ee, p->a_ei, p->a_ii, p->P, p->rhoE, p->rE, p->rI, p->mu, p->sigmaI, p->sqdtD, p->dtSim,
+                       p->tauE, p->tauI, tau_ip);
     a.keys = keys; a.G = G; a.sigmaE = sigmaE; a.E = E; a.I = I; a.A = A;
     a.recE = recE; a.recI = recI; a.recA = recA; a.rec_ld = rec_ld; a.rec_every = rec_every;
     a.step0 = step0; a.nsteps = nsteps;
