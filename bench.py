@@ -235,7 +235,8 @@ def main():
         try:
             d = json.load(open(pmc))
             if d.get("B") == B and d.get("N") == N and d.get("euler_steps") == EULER and \
-                    d.get("precision") == args.precision:
+                    d.get("precision") == args.precision and \
+                    (N <= 96 or ("persist" in d.get("kernel", "")) == (os.environ.get("WCSDE_PERSISTENT") != "0")):
                 pmc_d = d
         except (ValueError, OSError):
             pmc_d = {}
@@ -267,20 +268,32 @@ def main():
         gbps = per_launch_ns * 24 / t_launch / 1e9
         roof["state_streaming_equiv"] = {"bytes_per_node_step": 24, "GBps": gbps, "x_hbm_peak": gbps / PEAK_HBM_GBPS}
     else:
-        # C5 (step_kernel): one launch per Euler step, the state streams through HBM / Infinity Cache each
-        # step -- priced against HBM at the algorithmic 24 B per node-step (fp32 E, I, a_ie read + written)
-        achieved = per_launch_ns * 24 / t_launch / 1e9
-        roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic, "traffic_algorithmic": per_launch_ns * 24,
-                "kernel": "step_kernel (wc_sde_large.hip; %d launches of 1 Euler step, %d sims)" % (EULER, B),
-                "algorithmic_bytes_per_node_step": 24,
+        # C5 (persist_kernel, wc_sde_large.hip): one launch integrates the whole chunk with the state in
+        # registers; each Euler step is a 1024 x 2560 x 1024 fp16x3 GEMM whose operands stream from
+        # L2 / Infinity Cache (the E image handed over between the node-block workgroups every step).
+        # Priced against the fp16 MFMA that runs the contraction (the work actually issued, padding
+        # included); the operand stream that binds it is reported beside
+        ifl = issued_mfma_flops_per_node_step(N)
+        achieved = per_launch_ns * ifl / t_launch / 1e12
+        Np, Bp = -(-N // 128) * 128, -(-B // 80) * 80
+        stream = (Np // 128) * (Bp // 80) * (128 + 80) * Np * 4  # operand bytes per step (A rows + E image)
+        roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / PEAK_F16_TFLOPS, "traffic": traffic,
+                "traffic_algorithmic": per_launch_ns * 24,
+                "kernel": "persist_kernel (wc_sde_large.hip; one launch = %d Euler steps of %d sims, state in "
+                          "registers)" % (EULER, B),
                 "algorithmic_flops_per_node_step": fl,
+                "issued_f16_flops_per_node_step": ifl,
                 "algorithmic_tflops_fp32_equiv": per_launch_ns * fl / t_launch / 1e12,
-                "note": "traffic = PMC FETCH+WRITE per launch (includes Infinity-Cache hits): the kernel moves "
-                        "36 B of state per node-step plus the per-XCD connectome and E-image fetches"}
+                "operand_stream": {"bytes_per_step": stream,
+                                   "GBps": stream * EULER / t_launch / 1e9},
+                "note": "fp16 MFMA roofline of the issued coupling work; the kernel is bound by the per-step "
+                        "operand stream from L2/Infinity Cache (operand_stream; ablation: 15 of 28 us per step). "
+                        "traffic = PMC FETCH+WRITE per launch; traffic_algorithmic = 24 B per node-step of "
+                        "state streaming, which this kernel no longer moves"}
     roof["kernel_ms_per_launch"] = kern["sde"]
     roof["pmc"] = util or None
-    roof["issued_mfma"] = issued
+    roof["issued_mfma"] = issued if N <= 96 else None
     out = {
         "metric": "node-timesteps/sec (90-node WC, (G,sigma)x50-seed sweep) at 1/2/4/8 GPUs"
                   + ("" if args.config == "c3" else " [config 5: 1000-node synthetic connectome]"),

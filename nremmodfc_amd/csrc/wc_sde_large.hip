@@ -682,6 +682,9 @@ __host__ __device__ __forceinline__ uint32_t pimg_unit(const PGeo& g, int c, int
     return (uint32_t)((((size_t)c * g.SBp + sb) * kParts + p) * kPT + t);
 }
 
+// DIAG (timing ablations only, WCSDE_PERSISTENT=2..5; results are wrong): 1 = no MFMA, 2 = no
+// epilogue arithmetic, 3 = no K-loop operand loads, 4 = no hand-off waits
+template <int DIAG = 0>
 __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a) {
     typedef __attribute__((ext_vector_type(4))) float f4;
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -761,6 +764,10 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     // consumer: one lane polls the counter (relaxed, sc1 loads), then ONE agent acquire, a vmcnt
     // wait and a workgroup barrier before any wave loads the image (bounded: error word + exit)
     auto wait_for = [&](unsigned target) -> bool {
+        if (DIAG == 4) {
+            __syncthreads();
+            return true;
+        }
         if (tid == 0) {
             int ok = 0;
             for (uint32_t it = 0; it < kSpinLimit; ++it) {
@@ -801,6 +808,7 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     f16x8 fa[2][kParts];
     u4 rb[2][2];
     auto load_chunk = [&](int c, int slot, int buf) {
+        if (DIAG == 3) return;
         const f16x8* ap = asrc + (size_t)c * kParts * 64;
         fa[slot][0] = ap[0];
         fa[slot][1] = ap[64];
@@ -817,6 +825,10 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
             const f16x8 fb0 = ldsB[slot][t][lane], fb1 = ldsB[slot][kPT + t][lane];
+            if (DIAG == 1) {
+                acc[t][0] += (float)fb0[0] + (float)a0[0] + (float)fb1[1] + (float)a1[1];
+                continue;
+            }
             // small terms first (2^-11: lo.hi, hi.lo; 1: hi.hi), as in step_kernel
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, fb0, acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb1, acc[t], 0, 0, 0);
@@ -863,6 +875,11 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
                         if (a.recA) static_cast<float*>(a.recA)[o] = (float)Av[t][r].get();
                     }
                 }
+            }
+            if (DIAG == 2) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) E[t][r] += 1e-30f * acc[t][r];
+                continue;
             }
             float z[4];
             quad_normals_raw(gstep, (uint32_t)(4 * mt + gq), ldsK[16 * t + j], z);
@@ -919,19 +936,17 @@ int cu_count_large() {
     return n;
 }
 
-// OPT-IN (WCSDE_PERSISTENT=1): measured on MI355X it is no faster than step_kernel -- 33.7 vs
-// 32.8 us per step in the C5 bench pipeline (35.9 vs 38.0 with node-major ring records), and
-// 33.3 us at half the batch: the K loop waits 32 times per step on MALL-latency sc1 loads of the
-// freshly published E image, which the register budget (state + 20 accumulators at 2 waves per
-// SIMD) does not let it prefetch deeper.  It applies when every workgroup gets a
-// CU of its own (residency) and the image offsets fit the 32-bit buffer descriptors.
+// The product path for fp32 N > 96 whenever every workgroup gets a CU of its own (residency) and
+// the image offsets fit the 32-bit buffer descriptors.  C5 bench: 28.2 us per step against the
+// step kernel's 31.8.  WCSDE_PERSISTENT=0 forces step_kernel; 2..5 select the
+// timing ablations (wrong results).
 bool persistent_ok(int B, int N) {
     const char* env = getenv("WCSDE_PERSISTENT");
-    if (!env || env[0] != '1') return false;
+    if (env && (env[0] < '1' || env[0] > '5')) return false;
     const PGeo g = pgeometry(B, N);
     if (2 * (size_t)g.Np * g.Bp * 4 >= (size_t)INT32_MAX) return false;
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)persist_kernel, kPWaves * 64, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)persist_kernel<0>, kPWaves * 64, 0) != hipSuccess ||
         occ < 1)
         return false;
     return g.SBp * g.NBp <= cu_count_large();
@@ -963,7 +978,15 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
                        reinterpret_cast<f16x8*>(a.ws + g.o_frag));
     hipError_t me = hipMemsetAsync(a.ws + g.o_cnt, 0, g.o_err + al(4) - g.o_cnt, st);  // counters + error word
     if (me != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(me));
-    hipLaunchKernelGGL(persist_kernel, dim3((unsigned)(g.SBp * g.NBp)), dim3(kPWaves * 64), 0, st, a);
+    const dim3 grid((unsigned)(g.SBp * g.NBp)), blk(kPWaves * 64);
+    const char* env = getenv("WCSDE_PERSISTENT");
+    switch (env ? env[0] : '1') {
+        case '2': hipLaunchKernelGGL(persist_kernel<1>, grid, blk, 0, st, a); break;
+        case '3': hipLaunchKernelGGL(persist_kernel<2>, grid, blk, 0, st, a); break;
+        case '4': hipLaunchKernelGGL(persist_kernel<3>, grid, blk, 0, st, a); break;
+        case '5': hipLaunchKernelGGL(persist_kernel<4>, grid, blk, 0, st, a); break;
+        default: hipLaunchKernelGGL(persist_kernel<0>, grid, blk, 0, st, a);
+    }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
 }

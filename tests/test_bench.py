@@ -50,11 +50,12 @@ def test_bench_json_contract(cuda):
 
 
 @pytest.mark.gpu
-def test_bench_c5_line_priced_on_hbm(cuda):
+def test_bench_c5_line_priced_on_mfma(cuda):
     out = subprocess.run([sys.executable, "bench.py", "--config", "c5", "--steps", "1", "--warmup", "0",
                           "--sde-only"], cwd=ROOT, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stderr[-2000:]
     d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
     r = d["roofline"]
-    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1 and r["peak"] == 2500.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12 and r["operand_stream"]["GBps"] > 0
     assert d["config"]["nodes"] == 1000 and d["config"]["sims_per_gpu"] == 2500

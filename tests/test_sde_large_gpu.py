@@ -89,12 +89,14 @@ def test_large_f32_tracks_f64_statistics(cuda):
 
 
 def _both_paths(sc, G, S, keys, steps, rec_every=20, rec_ld=0, chunks=None):
-    """The same integration through the persistent kernel (opt-in, WCSDE_PERSISTENT=1) and through
-    the one-launch-per-step product kernel: final state and records."""
+    """The same integration through the default path (the persistent kernel wherever it is
+    resident) and through the one-launch-per-step kernel (WCSDE_PERSISTENT=0): final state and records."""
     import os
     out = {}
-    for flag in ("1", "0"):
-        os.environ["WCSDE_PERSISTENT"] = flag
+    for flag in ("default", "0"):
+        os.environ.pop("WCSDE_PERSISTENT", None)
+        if flag != "default":
+            os.environ["WCSDE_PERSISTENT"] = flag
         try:
             b = Batch(sc, G, S, keys, precision="f32")
             b.integrate(60, 0.05)
@@ -112,7 +114,7 @@ def _both_paths(sc, G, S, keys, steps, rec_every=20, rec_ld=0, chunks=None):
             out[flag] = (b.E.clone(), b.I.clone(), b.A.clone(), rec)
         finally:
             os.environ.pop("WCSDE_PERSISTENT", None)
-    return out["1"], out["0"]
+    return out["default"], out["0"]
 
 
 @pytest.mark.parametrize("N,B", [(1000, 2500), (250, 170), (97, 1)])
