@@ -632,11 +632,40 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
 constexpr int kPN = 128, kPS = 80, kPT = kPS / 16;  // nodes, simulations, simulation tiles per workgroup
 constexpr int kPWaves = kPN / 16;                     // 8
 constexpr uint32_t kSpinLimit = 1u << 22;             // polls per wait before giving up (~seconds)
+constexpr int kPRes = 8;  // K chunks of the connectome tile kept in LDS (128 KB of the 512 KB streamed per step)
 
 struct PGeo {
     int B, N, Np, Bp, MT, NC, SBp, NBp;
+    int nbx, gn, sbx;  // XCD placement: nbx node blocks x sbx simulation blocks per XCD (gn node groups); nbx = 0: plain order
     size_t o_frag, o_scl, o_x, o_cnt, o_err, total;
 };
+
+// blockIdx -> (simulation block, node block).  Workgroup b runs on XCD b % 8 (dispatch order;
+// used for speed only, nothing depends on it): each XCD gets nbx node blocks of sbx simulation
+// blocks, so its L2 holds nbx x 128 connectome rows across steps and each E-image line it
+// fetches is read by nbx workgroups
+void pplace(PGeo& g, int nbx) {
+    g.nbx = 0;
+    const int W = g.SBp * g.NBp;
+    if (nbx <= 0 || W % 8 || g.NBp % nbx) return;
+    const int gn = g.NBp / nbx;
+    if (8 % gn || g.SBp % (8 / gn)) return;
+    g.nbx = nbx;
+    g.gn = gn;
+    g.sbx = g.SBp / (8 / gn);
+}
+
+__device__ __forceinline__ void pblock(const PGeo& g, int& sb, int& nb) {
+    const int b = blockIdx.x;
+    if (g.nbx == 0) {
+        sb = b % g.SBp;
+        nb = b / g.SBp;
+        return;
+    }
+    const int x = b & 7, r = b >> 3;
+    nb = (x % g.gn) * g.nbx + r % g.nbx;
+    sb = (x / g.gn) * g.sbx + r / g.nbx;
+}
 
 PGeo pgeometry(int B, int N) {
     PGeo g{};
@@ -682,7 +711,7 @@ __host__ __device__ __forceinline__ uint32_t pimg_unit(const PGeo& g, int c, int
     return (uint32_t)((((size_t)c * g.SBp + sb) * kParts + p) * kPT + t);
 }
 
-// DIAG (timing ablations only, WCSDE_PERSISTENT=2..5; results are wrong): 1 = no MFMA, 2 = no
+// DIAG (timing ablations only, diag build, WCSDE_PERSISTENT=2..5; results are wrong): 1 = no MFMA, 2 = no
 // epilogue arithmetic, 3 = no K-loop operand loads, 4 = no hand-off waits
 template <int DIAG = 0>
 __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a) {
@@ -691,12 +720,14 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     // [stage][part x sim tile][lane] B (2 stages); per-simulation G, slope and keys.  The state and
     // the A fragments live in registers (~215 VGPRs: one workgroup per CU).
     __shared__ f16x8 ldsB[2][kParts * kPT][64];
+    __shared__ f16x8 ldsA[kPRes][kPWaves][kParts][64];  // the first kPRes K chunks of the connectome rows, resident
     __shared__ float2 ldsGS[kPS];
     __shared__ uint64_t ldsK[kPS];
     __shared__ int go, uni;
     const PGeo& g = a.g;
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, j = lane & 15, gq = lane >> 4;
-    const int sb = blockIdx.x % g.SBp, nb = blockIdx.x / g.SBp;
+    int sb, nb;
+    pblock(g, sb, nb);
     const int mt = nb * kPWaves + w;  // this wave's node tile
     const int n0 = 16 * mt + 4 * gq;
     const float* scl = reinterpret_cast<const float*>(a.ws + g.o_scl);
@@ -706,7 +737,6 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(a.ws + g.o_x, 0,
                                                                          (int)(2 * (size_t)g.Np * g.Bp * 4), 0x00020000);
     const uint32_t img_units = (uint32_t)((size_t)g.Np * g.Bp * 4 / 1024);  // 1-KB units (64 lanes x 16 B) per image
-    const f16x8* X = reinterpret_cast<const f16x8*>(a.ws + g.o_x);
 
     // ---- state into registers (step_kernel's prep_kernel arithmetic); G and slope per
     // simulation when this workgroup's cells do not vary by node (every sweep but the maps
@@ -755,11 +785,7 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     // consumer: one lane polls the counter (relaxed, sc1 loads), then ONE agent acquire, a vmcnt
     // wait and a workgroup barrier before any wave loads the image (bounded: error word + exit)
@@ -779,8 +805,6 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
                 __builtin_amdgcn_s_sleep(1);
             }
             if (!ok) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             go = ok;
         }
         __syncthreads();
@@ -804,23 +828,31 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     // to one of two LDS stages once they land
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
     const f16x8* asrc = F + (size_t)mt * g.NC * kParts * 64 + lane;
-    const u4* X4 = reinterpret_cast<const u4*>(X);
     f16x8 fa[2][kParts];
     u4 rb[2][2];
+    const int res = g.NC < kPRes ? g.NC : kPRes;  // chunks c < res come from ldsA (NC is a multiple of 4)
+    for (int c = 0; c < res; ++c) {
+        ldsA[c][w][0][lane] = asrc[(size_t)c * kParts * 64];
+        ldsA[c][w][1][lane] = asrc[(size_t)c * kParts * 64 + 64];
+    }
     auto load_chunk = [&](int c, int slot, int buf) {
         if (DIAG == 3) return;
-        const f16x8* ap = asrc + (size_t)c * kParts * 64;
-        fa[slot][0] = ap[0];
-        fa[slot][1] = ap[64];
-        const u4* xb = X4 + (size_t)(buf * img_units + pimg_unit(g, c, sb, 0, 0)) * 64;
-        rb[slot][0] = xb[tid];
-        if (tid < 128) rb[slot][1] = xb[512 + tid];
+        if (c >= res) {
+            const f16x8* ap = asrc + (size_t)c * kParts * 64;
+            fa[slot][0] = ap[0];
+            fa[slot][1] = ap[64];
+        }
+        const int xo = (int)(((buf * img_units + pimg_unit(g, c, sb, 0, 0)) * 64 + tid) * 16);
+        rb[slot][0] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 16));
+        if (tid < 128) rb[slot][1] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo + 512 * 16, 0, 16));
     };
     auto do_chunk = [&](int c, int slot, int buf, f4 (&acc)[kPT]) {
         reinterpret_cast<u4*>(&ldsB[slot][0][0])[tid] = rb[slot][0];
         if (tid < 128) reinterpret_cast<u4*>(&ldsB[slot][0][0])[512 + tid] = rb[slot][1];
         __syncthreads();  // stage `slot` was last read at chunk c - 2, before the previous barrier
-        const f16x8 a0 = fa[slot][0], a1 = fa[slot][1];
+        // (each wave reads only its own ldsA slice, written by itself before the step loop)
+        const f16x8 a0 = c < res ? ldsA[c][w][0][lane] : fa[slot][0];
+        const f16x8 a1 = c < res ? ldsA[c][w][1][lane] : fa[slot][1];
         if (c + 2 < g.NC) load_chunk(c + 2, slot, buf);
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
@@ -938,8 +970,8 @@ int cu_count_large() {
 
 // The product path for fp32 N > 96 whenever every workgroup gets a CU of its own (residency) and
 // the image offsets fit the 32-bit buffer descriptors.  C5 bench: 28.2 us per step against the
-// step kernel's 31.8.  WCSDE_PERSISTENT=0 forces step_kernel; 2..5 select the
-// timing ablations (wrong results).
+// step kernel's 31.8.  WCSDE_PERSISTENT=0 forces step_kernel; in the diag build
+// (libwcsde_diag.so) 2..5 select the timing ablations (wrong results).
 bool persistent_ok(int B, int N) {
     const char* env = getenv("WCSDE_PERSISTENT");
     if (env && (env[0] < '1' || env[0] > '5')) return false;
@@ -964,6 +996,8 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
     a.step0 = step0; a.nsteps = nsteps;
     a.ws = static_cast<char*>(workspace);
     a.g = pgeometry(B, N);
+    const char* pm = getenv("WCSDE_PMAP");
+    pplace(a.g, pm ? atoi(pm) : 0);
     const PGeo& g = a.g;
     // connectome image in the 128-node padding (frag_f16_kernel takes a Geo)
     Geo fg{};
@@ -979,6 +1013,7 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
     hipError_t me = hipMemsetAsync(a.ws + g.o_cnt, 0, g.o_err + al(4) - g.o_cnt, st);  // counters + error word
     if (me != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(me));
     const dim3 grid((unsigned)(g.SBp * g.NBp)), blk(kPWaves * 64);
+#ifdef WCSDE_DIAG
     const char* env = getenv("WCSDE_PERSISTENT");
     switch (env ? env[0] : '1') {
         case '2': hipLaunchKernelGGL(persist_kernel<1>, grid, blk, 0, st, a); break;
@@ -987,6 +1022,9 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
         case '5': hipLaunchKernelGGL(persist_kernel<4>, grid, blk, 0, st, a); break;
         default: hipLaunchKernelGGL(persist_kernel<0>, grid, blk, 0, st, a);
     }
+#else
+    hipLaunchKernelGGL(persist_kernel<0>, grid, blk, 0, st, a);
+#endif
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
 }
