@@ -22,7 +22,7 @@ def main():
     keys = sim_keys(np.arange(B) % 50, np.arange(B) // 50)
     ring = torch.empty(B * N * (steps // 20), dtype=torch.float32, device="cuda")
     ref = None
-    for rep in range(2):
+    for rep in range(int(os.environ.get("REPS", "2"))):
         for pm in (sys.argv[2] if len(sys.argv) > 2 else "0,1,2,4,8").split(","):
             os.environ["WCSDE_PMAP"] = pm
             b = Batch(sc, G, S, keys, precision="f32")
@@ -37,7 +37,7 @@ def main():
             ref = st if ref is None else ref
             print(f"rep {rep} pmap {pm}: {dt / steps * 1e6:.2f} us/step, {B * N * steps / dt:.3e} node-steps/s, "
                   f"same={same}", flush=True)
-            assert same
+            assert same or os.environ.get("WCSDE_PERSISTENT", "1") != "1"  # 2..5: diag-build ablations
 
 
 if __name__ == "__main__":
