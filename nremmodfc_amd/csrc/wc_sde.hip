@@ -143,6 +143,54 @@ __global__ void build_frag_f16(const double* __restrict__ sc, int N, const float
     for (int p = 0; p < 2; ++p) frag[(size_t)(tc * 2 + p) * 64 + lane] = part[p];
 }
 
+// ---------------- packed fp32 cell pair (the fp32 product update) ----------------
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct PkConsts {
+    f2v a_ee, Pm, knoise, cIe, cIi, cI0, rE, rI, dtE, dtI, dtA, rhoE;
+};
+
+// Two cells of the folded-constant fp32 update (wc:77-83; the scalar form is in wc_sde_kernel's
+// kFast branch) as packed fp32 math: v_pk_fma/mul/add_f32 carry two cells per instruction and
+// round exactly like their scalar forms, the transcendentals stay scalar.  Same operations in
+// the same order as the scalar form, so the same bits.
+#pragma clang fp contract(off)
+__device__ __forceinline__ void cell_pair_f32(const PkConsts& k, f2v& e, f2v& in, f2v& ahi, f2v& alo, f2v cpl,
+                                              f2v G, f2v sl, f2v z) {
+    const f2v e0 = e, in0 = in;
+    f2v x = __builtin_elementwise_fma(k.a_ee, e0, k.Pm);
+    x = __builtin_elementwise_fma(-ahi, in0, x);
+    x = __builtin_elementwise_fma(G, cpl, x);
+    x = __builtin_elementwise_fma(k.knoise, z, x);
+    const f2v te = x * sl;
+    const f2v de = 1.0f + f2v{__builtin_amdgcn_exp2f(te.x), __builtin_amdgcn_exp2f(te.y)};
+    const f2v SE = {__builtin_amdgcn_rcpf(de.x), __builtin_amdgcn_rcpf(de.y)};
+    const f2v ti = __builtin_elementwise_fma(e0, k.cIe, __builtin_elementwise_fma(in0, k.cIi, k.cI0));
+    const f2v di = 1.0f + f2v{__builtin_amdgcn_exp2f(ti.x), __builtin_amdgcn_exp2f(ti.y)};
+    const f2v SI = {__builtin_amdgcn_rcpf(di.x), __builtin_amdgcn_rcpf(di.y)};
+    const f2v one = {1.0f, 1.0f};
+    // (a_ie first: e0 and in0 are last read by their own updates, which can then write in place)
+    const f2v tA = in0 * k.dtA;
+    const f2v inc = __builtin_elementwise_fma(e0, tA, -k.rhoE * tA);
+    const f2v t = inc + alo;  // Kahan-Babuska, as AccA<true>::add
+    const f2v s = ahi + t;
+    alo = t - (s - ahi);
+    ahi = s;
+    e = __builtin_elementwise_fma(k.dtE, __builtin_elementwise_fma(__builtin_elementwise_fma(-k.rE, e0, one), SE, -e0), e0);
+    in = __builtin_elementwise_fma(k.dtI, __builtin_elementwise_fma(__builtin_elementwise_fma(-k.rI, in0, one), SI, -in0), in0);
+}
+
+// quad_normals_raw with the radius products packed: (z0, z1), (z2, z3)
+__device__ __forceinline__ void quad_normals_pk(uint64_t step, uint32_t q, uint64_t key, f2v z[2]) {
+    uint32_t x[4];
+    philox_ctr(step, q, key, x);
+    const float r0 = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u01f_fast(x[0])));
+    const float r1 = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u01f_fast(x[2])));
+    const float a0 = u01f_fast(x[1]), a1 = u01f_fast(x[3]);
+    z[0] = f2v{__builtin_amdgcn_cosf(a0), __builtin_amdgcn_sinf(a0)} * r0;
+    z[1] = f2v{__builtin_amdgcn_cosf(a1), __builtin_amdgcn_sinf(a1)} * r1;
+}
+#pragma clang fp contract(on)
+
 // ---------------- variants ----------------
 enum : int {
     V_FRAG_REGS = 1,  // A-operand fragments held in registers (else streamed from LDS each step)
@@ -157,6 +205,7 @@ enum : int {
     V_ZFIRST = 1024,  // fp32 fast path: the step's normals drawn before the coupling MFMAs
     V_ILV = 2048,     // ... interleaved with them (sched_group_barrier: 1 MFMA, 6 VALU)
     V_ILV2 = 4096,    // ... interleaved with them (1 MFMA, 2 VALU: the free half of a 16x16x32 gap)
+    V_SCALAR = 8192,  // ablation: the fp32 fast update one cell per instruction (round-2 form)
 };
 
 // SG > 1: one workgroup holds SG groups of 16 simulations (SG x NW waves) that
@@ -182,6 +231,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     // fp32 with the compensated a_ie: the folded-constant update (Sl holds -sigmaE log2 e)
     constexpr bool kFast = sizeof(Real) == 4 && kPairA;
     constexpr bool kZFirst = kFast && kRng && (VAR & V_ZFIRST) != 0;
+    constexpr bool kPk = (VAR & V_SCALAR) == 0;  // packed fp32 cell pairs (cell_pair_f32)
     // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
     constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
     constexpr int kFragUnits = kBf ? NT * NC * PS : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
@@ -320,6 +370,12 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     const Real dt = (Real)a.dtSim;
     const Real dtA = (Real)(a.dtSim / a.tau_ip);
     const Real tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;  // fp64 exact forms
+    PkConsts pk{};
+    if constexpr (kFast && kPk) {
+        auto bc = [](float v) { return f2v{v, v}; };
+        pk = PkConsts{bc((float)a_ee), bc(Pm), bc(knoise), bc(cIe), bc(cIi), bc(cI0), bc((float)rE), bc((float)rI),
+                      bc((float)dtE), bc((float)dtI), bc((float)dtA), bc((float)rhoE)};
+    }
     const size_t BN = (size_t)a.B * N;
     const int rec_every = (int)a.rec_every;
     int rec_cnt = 0, rec_row = 0;
@@ -475,6 +531,32 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         for (int u = 0; u < OT; ++u) {
             if constexpr (sizeof(Real) == 8) __builtin_amdgcn_sched_barrier(0);  // fp64: bound live ranges
             Real z[4] = {0, 0, 0, 0};
+            if constexpr (kFast && kPk) {
+                f2v zp[2] = {f2v{0, 0}, f2v{0, 0}};
+                if constexpr (kZFirst) {
+                    zp[0] = f2v{zz[u][0], zz[u][1]};
+                    zp[1] = f2v{zz[u][2], zz[u][3]};
+                } else if constexpr (kRng) {
+                    quad_normals_pk(gstep, (uint32_t)(4 * (T0 + u) + g), key, zp);
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int r = 2 * h;
+                    f2v e = {E[u][r], E[u][r + 1]}, in = {I[u][r], I[u][r + 1]};
+                    f2v ahi = {A[u][r].hi, A[u][r + 1].hi}, alo = {A[u][r].lo, A[u][r + 1].lo};
+                    const f2v cpl = kMfma ? f2v{acc[u][r], acc[u][r + 1]} : e;
+                    cell_pair_f32(pk, e, in, ahi, alo, cpl, f2v{Gc[u][r], Gc[u][r + 1]}, f2v{Sl[u][r], Sl[u][r + 1]}, zp[h]);
+                    E[u][r] = e.x;
+                    E[u][r + 1] = e.y;
+                    I[u][r] = in.x;
+                    I[u][r + 1] = in.y;
+                    A[u][r].hi = ahi.x;
+                    A[u][r + 1].hi = ahi.y;
+                    A[u][r].lo = alo.x;
+                    A[u][r + 1].lo = alo.y;
+                }
+                continue;
+            }
             if constexpr (kFast) {
                 if constexpr (kZFirst) {
 #pragma unroll
@@ -747,6 +829,8 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 34: return launch_v<float, 6, 6, V_F16X3 | K>(ka, sc, ws, st);
         case 35: return launch_v<float, 6, 6, V_F16X3 | V_FRAG_REGS | K | V_ZFIRST | V_ILV2>(ka, sc, ws, st);
         case 36: return launch_v<float, 6, 2, V_F16X3 | V_FRAG_REGS | K | V_ZFIRST>(ka, sc, ws, st);
+        // 37: the C3 product configuration (SG = 5, paired records) with the round-2 one-cell-per-instruction update
+        case 37: return launch_v<float, 6, 3, V_F16X3 | K | V_REC2 | V_SCALAR, 1, 5>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
