@@ -93,6 +93,20 @@ __device__ __forceinline__ void quad_normals_raw(uint64_t step, uint32_t q, uint
     z[3] = r1 * __builtin_amdgcn_sinf(a1);
 }
 
+// packed fp32 pair (v_pk_fma/mul/add_f32: two cells per instruction, each rounded like its scalar form)
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// quad_normals_raw with the radius products packed: (z0, z1), (z2, z3) -- the same bits
+__device__ __forceinline__ void quad_normals_pk(uint64_t step, uint32_t q, uint64_t key, f2v z[2]) {
+    uint32_t x[4];
+    philox_ctr(step, q, key, x);
+    const float r0 = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u01f_fast(x[0])));
+    const float r1 = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u01f_fast(x[2])));
+    const float a0 = u01f_fast(x[1]), a1 = u01f_fast(x[3]);
+    z[0] = f2v{__builtin_amdgcn_cosf(a0), __builtin_amdgcn_sinf(a0)} * r0;
+    z[1] = f2v{__builtin_amdgcn_cosf(a1), __builtin_amdgcn_sinf(a1)} * r1;
+}
+
 // fp32 standard normals (test hook, N > 96 path)
 __device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, float z[4]) {
     quad_normals_raw(step, q, key, z);

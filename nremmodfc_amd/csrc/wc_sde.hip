@@ -144,7 +144,6 @@ __global__ void build_frag_f16(const double* __restrict__ sc, int N, const float
 }
 
 // ---------------- packed fp32 cell pair (the fp32 product update) ----------------
-typedef float f2v __attribute__((ext_vector_type(2)));
 struct PkConsts {
     f2v a_ee, Pm, knoise, cIe, cIi, cI0, rE, rI, dtE, dtI, dtA, rhoE;
 };
@@ -179,16 +178,6 @@ __device__ __forceinline__ void cell_pair_f32(const PkConsts& k, f2v& e, f2v& in
     in = __builtin_elementwise_fma(k.dtI, __builtin_elementwise_fma(__builtin_elementwise_fma(-k.rI, in0, one), SI, -in0), in0);
 }
 
-// quad_normals_raw with the radius products packed: (z0, z1), (z2, z3)
-__device__ __forceinline__ void quad_normals_pk(uint64_t step, uint32_t q, uint64_t key, f2v z[2]) {
-    uint32_t x[4];
-    philox_ctr(step, q, key, x);
-    const float r0 = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u01f_fast(x[0])));
-    const float r1 = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u01f_fast(x[2])));
-    const float a0 = u01f_fast(x[1]), a1 = u01f_fast(x[3]);
-    z[0] = f2v{__builtin_amdgcn_cosf(a0), __builtin_amdgcn_sinf(a0)} * r0;
-    z[1] = f2v{__builtin_amdgcn_cosf(a1), __builtin_amdgcn_sinf(a1)} * r1;
-}
 #pragma clang fp contract(on)
 
 // ---------------- variants ----------------
