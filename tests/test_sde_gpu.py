@@ -231,3 +231,24 @@ def test_f32_shapes_and_tails(cuda, N, B):
     observed(d, f"shapes-{N}-{B}")
     # observed max <= 1.5e-7, rms <= 2.5e-8 (300 steps)
     assert d.max() <= 2e-6 and np.sqrt(np.mean(d ** 2)) <= 3e-7, (d.max(), np.sqrt(np.mean(d ** 2)))
+
+
+@pytest.mark.parametrize("rel", [2.0 ** -11, -(2.0 ** -11), 2.0 ** -14])
+def test_f32_gate_detects_coupling_error(cuda, sc90, rel):
+    """The fp32 gate bites: a coupling off by 2^-11 relative (what dropping the fp16 split's lo
+    term, or mis-scaling it, would cost) or by 2^-14 moves the 300-step trajectories past the
+    300-step bound that the product passes (test_f32_shapes_and_tails: max 2e-6, rms 3e-7).  The
+    error is injected as G (1 + rel) on the device side only: G multiplies the coupling alone."""
+    B = 16
+    keys = sim_keys(list(range(B)), [90] * B)
+    G = np.full(B, 0.16)
+    gb = Batch(sc90, G * (1 + rel), 7.68, keys, precision="f32")
+    ob = oracle.OracleBatch(sc90, G, 7.68, keys, driver_params())
+    gb.integrate(100, 0.05)
+    ob.integrate(100, 0.05)
+    rec = torch.empty((10, B, 90), dtype=torch.float32, device="cuda")
+    gb.integrate(200, 2.0, 20, rec)
+    o = ob.integrate(200, 2.0, 20)
+    d = np.abs(rec.double().cpu().numpy().transpose(1, 0, 2) - o)
+    mx, rms = observed(d, f"gate-coupling-{rel:+.1e}")
+    assert mx > 2e-6 or rms > 3e-7, (mx, rms)
