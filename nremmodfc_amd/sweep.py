@@ -176,8 +176,11 @@ def run_sims(sims: List[Sim], sc, empfcs, schedule=None, precision="f32", batch=
 
 
 class Progress:
-    """Progress lines about once a minute (synchronising the device so the line
-    reflects finished work, not just queued launches)."""
+    """Progress lines about once a minute.  Every call (one per launch: <= 500k Euler steps, a
+    recorded chunk) synchronises the device, so the host never queues more than one launch
+    ahead and the line reflects finished work: a persistent launch integrates its whole range
+    in one kernel, so without the wait the host would queue the sweep in milliseconds and stay
+    silent until the end."""
 
     def __init__(self, rank, every_s=60.0):
         import time
@@ -187,10 +190,10 @@ class Progress:
     def __call__(self, phase, step, total):
         import time
         import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
         now = time.perf_counter()
         if now - self.last >= self.every:
-            torch.cuda.synchronize()
-            now = time.perf_counter()
             print(f"[rank {self.rank}] {phase}: step {step}/{total} ({100 * step / total:.1f}%), "
                   f"{now - self.t0:.0f} s", flush=True)
             self.last = now
