@@ -5,7 +5,7 @@ heatmaps.py cannot be imported here (seaborn, matplotlib at module top), so its 
 reproduces the optima run_many_seeds.py:34-38 quotes for the homogeneous model when applied to
 the shipped table (tests/golden/shipped_heatmaps.npz, made by make_heatmap_golden.py).
 
-Applied to this build's full homogeneous sweep (profiles/r01_homo_sweep.txt.gz: 20,000
+Applied to this build's full homogeneous sweep (profiles/r02_homo_sweep.txt.gz: 20,000
 simulations x 1001 s, read with pandas exactly as heatmaps.py reads output/*.txt) it must give
 euccorr maps that track the shipped ones cell by cell, and the same W optimum.
 """
@@ -58,7 +58,7 @@ def test_restated_consumer_gives_the_reference_optima():
 
 
 def test_heatmaps_on_this_builds_full_sweep():
-    ours = extract(pd.read_csv(os.path.join(ROOT, "profiles", "r01_homo_sweep.txt.gz")))
+    ours = extract(pd.read_csv(os.path.join(ROOT, "profiles", "r02_homo_sweep.txt.gz")))
     g = np.load(os.path.join(ROOT, "tests", "golden", "shipped_heatmaps.npz"))
     np.testing.assert_allclose(ours["x_vals"], g["x_vals"])
     np.testing.assert_allclose(ours["y_vals"], g["y_vals"])
