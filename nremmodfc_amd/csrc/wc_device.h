@@ -185,12 +185,15 @@ __device__ __forceinline__ void split3(const float v[4], bf16x4& hi, bf16x4& mid
 // lo = fp16(x - hi) in one v_fma_mix{lo,hi}_f16 per value: x (fp32) * 1 - hi (read as
 // fp16), rounded once to fp16; x - hi is exact in fp32, so the result is the same as
 // converting hi back, subtracting and converting (two ops fewer per pair)
+// PRE: v is already E 2^10 (the N <= 96 product kernels keep E in those units, so the
+// split needs no scaling multiply)
+template <bool PRE = false>
 __device__ __forceinline__ void split2h(const float v[4], f16x4& hi, f16x4& lo) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-        const f2 x = (f2){v[2 * p], v[2 * p + 1]} * 1024.0f;
+        const f2 x = PRE ? (f2){v[2 * p], v[2 * p + 1]} : (f2){v[2 * p], v[2 * p + 1]} * 1024.0f;
         const h2 h = __builtin_convertvector(x, h2);
         uint32_t lb;
         asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lb) : "v"(x[0]), "v"(h));

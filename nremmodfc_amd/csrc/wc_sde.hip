@@ -145,14 +145,26 @@ __global__ void build_frag_f16(const double* __restrict__ sc, int N, const float
 
 // ---------------- packed fp32 cell pair (the fp32 product update) ----------------
 struct PkConsts {
-    f2v a_ee, Pm, knoise, cIe, cIi, cI0, rE, rI, dtE, dtI, dtA, rhoE;
+    f2v a_ee, Pm, knoise, cIe, cIi, cI0, rE, rI, dtE, dtI, dtA, rhoE, cA;
 };
 
 // Two cells of the folded-constant fp32 update (wc:77-83; the scalar form is in wc_sde_kernel's
 // kFast branch) as packed fp32 math: v_pk_fma/mul/add_f32 carry two cells per instruction and
 // round exactly like their scalar forms, the transcendentals stay scalar.  Same operations in
 // the same order as the scalar form, so the same bits.
+//
+// ES: e is E 2^10 (the units of the MFMA operand split, which then needs no scaling multiply).
+// The host scales a_ee, rE, cIe and dtA by 2^-10 and rhoE by 2^10 (exact), and the sigmoid
+// returns SE 2^10 as rcp(2^-10 (1 + 2^te)), the denominator by one fma with 2^-10 (exact), so
+// every rounding is the unscaled form's times 2^10: the same trajectory bit for bit (the
+// hardware reciprocal is exponent-transparent; tools/cmp_libs.py checks the bits).
+// WC_INC2 (default): the a_ie increment as in (E dtA - rhoE dtA), two operations instead of
+// three (WC_INC2=0: the round-2 form in (E tA - rhoE tA), tA = in dtA; -2.5% per C3 launch).
+#ifndef WC_INC2
+#define WC_INC2 1
+#endif
 #pragma clang fp contract(off)
+template <bool ES = false>
 __device__ __forceinline__ void cell_pair_f32(const PkConsts& k, f2v& e, f2v& in, f2v& ahi, f2v& alo, f2v cpl,
                                               f2v G, f2v sl, f2v z) {
     const f2v e0 = e, in0 = in;
@@ -161,19 +173,26 @@ __device__ __forceinline__ void cell_pair_f32(const PkConsts& k, f2v& e, f2v& in
     x = __builtin_elementwise_fma(G, cpl, x);
     x = __builtin_elementwise_fma(k.knoise, z, x);
     const f2v te = x * sl;
-    const f2v de = 1.0f + f2v{__builtin_amdgcn_exp2f(te.x), __builtin_amdgcn_exp2f(te.y)};
+    const f2v ex = {__builtin_amdgcn_exp2f(te.x), __builtin_amdgcn_exp2f(te.y)};
+    const f2v one = {1.0f, 1.0f};
+    constexpr float kS = ES ? 0x1p-10f : 1.0f;
+    const f2v de = ES ? __builtin_elementwise_fma(ex, f2v{kS, kS}, f2v{kS, kS}) : one + ex;
     const f2v SE = {__builtin_amdgcn_rcpf(de.x), __builtin_amdgcn_rcpf(de.y)};
     const f2v ti = __builtin_elementwise_fma(e0, k.cIe, __builtin_elementwise_fma(in0, k.cIi, k.cI0));
     const f2v di = 1.0f + f2v{__builtin_amdgcn_exp2f(ti.x), __builtin_amdgcn_exp2f(ti.y)};
     const f2v SI = {__builtin_amdgcn_rcpf(di.x), __builtin_amdgcn_rcpf(di.y)};
-    const f2v one = {1.0f, 1.0f};
     // (a_ie first: e0 and in0 are last read by their own updates, which can then write in place)
+#if WC_INC2
+    const f2v inc = in0 * __builtin_elementwise_fma(e0, k.dtA, k.cA);
+#else
     const f2v tA = in0 * k.dtA;
     const f2v inc = __builtin_elementwise_fma(e0, tA, -k.rhoE * tA);
+#endif
     const f2v t = inc + alo;  // Kahan-Babuska, as AccA<true>::add
     const f2v s = ahi + t;
     alo = t - (s - ahi);
     ahi = s;
+    // (ES: SE and e0 both carry 2^10, rE 2^-10: the same roundings times 2^10)
     e = __builtin_elementwise_fma(k.dtE, __builtin_elementwise_fma(__builtin_elementwise_fma(-k.rE, e0, one), SE, -e0), e0);
     in = __builtin_elementwise_fma(k.dtI, __builtin_elementwise_fma(__builtin_elementwise_fma(-k.rI, in0, one), SI, -in0), in0);
 }
@@ -221,6 +240,10 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr bool kFast = sizeof(Real) == 4 && kPairA;
     constexpr bool kZFirst = kFast && kRng && (VAR & V_ZFIRST) != 0;
     constexpr bool kPk = (VAR & V_SCALAR) == 0;  // packed fp32 cell pairs (cell_pair_f32)
+    // the fp16x3 packed product path keeps E in units of 2^-10 (E[][] holds E 2^10): the
+    // MFMA operand split needs no scaling multiply (cell_pair_f32<true>)
+    constexpr bool kEs = kFast && kPk && kHf;
+    constexpr float kEsc = kEs ? 1024.0f : 1.0f, kEinv = kEs ? 0x1p-10f : 1.0f;
     // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
     constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
     constexpr int kFragUnits = kBf ? NT * NC * PS : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
@@ -286,7 +309,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             const int n = 16 * (T0 + u) + 4 * g + r;
             const bool ok = n < N;
             const size_t o = (size_t)bb * N + (ok ? n : 0);
-            E[u][r] = ok ? (Real)a.E[o] : (Real)0;
+            E[u][r] = ok ? (Real)a.E[o] * (Real)kEsc : (Real)0;
             I[u][r] = ok ? (Real)a.I[o] : (Real)0;
             A[u][r].set(ok ? a.A[o] : 0.0);
             if constexpr (kParamRegs) {
@@ -308,8 +331,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 for (int c = 0; c < NC; ++c) {
                     bf16x4 h0, m0, l0, h1, m1, l1;
                     if constexpr (kHf) {
-                        split2h(E[2 * c], reinterpret_cast<f16x4&>(h0), reinterpret_cast<f16x4&>(m0));
-                        split2h(E[2 * c + 1], reinterpret_cast<f16x4&>(h1), reinterpret_cast<f16x4&>(m1));
+                        split2h<kEs>(E[2 * c], reinterpret_cast<f16x4&>(h0), reinterpret_cast<f16x4&>(m0));
+                        split2h<kEs>(E[2 * c + 1], reinterpret_cast<f16x4&>(h1), reinterpret_cast<f16x4&>(m1));
                     } else {
                         split3(E[2 * c], h0, m0, l0);
                         split3(E[2 * c + 1], h1, m1, l1);
@@ -331,7 +354,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 for (int u = 0; u < OT; ++u) {
                     const int t = T0 + u;  // chunk t/2, half t&1 (runtime: address arithmetic only)
                     bf16x4 hmo[3];
-                    if constexpr (kHf) split2h(E[u], reinterpret_cast<f16x4&>(hmo[0]), reinterpret_cast<f16x4&>(hmo[1]));
+                    if constexpr (kHf) split2h<kEs>(E[u], reinterpret_cast<f16x4&>(hmo[0]), reinterpret_cast<f16x4&>(hmo[1]));
                     else split3(E[u], hmo[0], hmo[1], hmo[2]);
 #pragma unroll
                     for (int p = 0; p < NP; ++p) x4[(((t >> 1) * PS + p) * 64 + lane) * 2 + (t & 1)] = hmo[p];
@@ -362,8 +385,10 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     PkConsts pk{};
     if constexpr (kFast && kPk) {
         auto bc = [](float v) { return f2v{v, v}; };
-        pk = PkConsts{bc((float)a_ee), bc(Pm), bc(knoise), bc(cIe), bc(cIi), bc(cI0), bc((float)rE), bc((float)rI),
-                      bc((float)dtE), bc((float)dtI), bc((float)dtA), bc((float)rhoE)};
+        // (kEs: E-side constants carry 2^-10, rhoE 2^10, all exact)
+        pk = PkConsts{bc((float)a_ee * kEinv), bc(Pm), bc(knoise), bc(cIe * kEinv), bc(cIi), bc(cI0),
+                      bc((float)rE * kEinv), bc((float)rI), bc((float)dtE), bc((float)dtI),
+                      bc((float)dtA * kEinv), bc((float)rhoE * kEsc), bc((float)(-a.rhoE * a.dtSim / a.tau_ip))};
     }
     const size_t BN = (size_t)a.B * N;
     const int rec_every = (int)a.rec_every;
@@ -391,10 +416,10 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                                                     (rec_row - (RB - 1));
                                         if constexpr (RB == 4) {
                                             *reinterpret_cast<real4*>(dst) =
-                                                real4{rbuf[u][r][0], rbuf[u][r][1], rbuf[u][r][2], E[u][r]};
+                                                real4{rbuf[u][r][0], rbuf[u][r][1], rbuf[u][r][2], E[u][r] * (Real)kEinv};
                                         } else {
                                             typedef __attribute__((ext_vector_type(2))) Real real2;
-                                            *reinterpret_cast<real2*>(dst) = real2{rbuf[u][r][0], E[u][r]};
+                                            *reinterpret_cast<real2*>(dst) = real2{rbuf[u][r][0], E[u][r] * (Real)kEinv};
                                         }
                                     }
                                 }
@@ -406,7 +431,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                             for (int r = 0; r < 4; ++r) {
 #pragma unroll
                                 for (int k = 0; k + 1 < RB - 1; ++k) rbuf[u][r][k] = rbuf[u][r][k + 1];
-                                rbuf[u][r][RB - 2] = E[u][r];
+                                rbuf[u][r][RB - 2] = E[u][r] * (Real)kEinv;
                             }
                     }
                 } else if (live) {
@@ -418,7 +443,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                             if (n < N) {
                                 const size_t cc = (size_t)bb * N + n;
                                 const size_t o = a.rec_ld ? cc * a.rec_ld + rec_row : (size_t)rec_row * BN + cc;
-                                static_cast<Real*>(a.recE)[o] = E[u][r];
+                                static_cast<Real*>(a.recE)[o] = E[u][r] * (Real)kEinv;
                                 if (a.recI) static_cast<Real*>(a.recI)[o] = I[u][r];
                                 if (a.recA) static_cast<Real*>(a.recA)[o] = (Real)A[u][r].get();
                             }
@@ -533,8 +558,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     const int r = 2 * h;
                     f2v e = {E[u][r], E[u][r + 1]}, in = {I[u][r], I[u][r + 1]};
                     f2v ahi = {A[u][r].hi, A[u][r + 1].hi}, alo = {A[u][r].lo, A[u][r + 1].lo};
-                    const f2v cpl = kMfma ? f2v{acc[u][r], acc[u][r + 1]} : e;
-                    cell_pair_f32(pk, e, in, ahi, alo, cpl, f2v{Gc[u][r], Gc[u][r + 1]}, f2v{Sl[u][r], Sl[u][r + 1]}, zp[h]);
+                    const f2v cpl = kMfma ? f2v{acc[u][r], acc[u][r + 1]} : e * kEinv;
+                    cell_pair_f32<kEs>(pk, e, in, ahi, alo, cpl, f2v{Gc[u][r], Gc[u][r + 1]}, f2v{Sl[u][r], Sl[u][r + 1]}, zp[h]);
                     E[u][r] = e.x;
                     E[u][r + 1] = e.y;
                     I[u][r] = in.x;
@@ -570,8 +595,12 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                         1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(e, cIe, __builtin_fmaf(in, cIi, cI0))));
                     E[u][r] = __builtin_fmaf(dtE, __builtin_fmaf(__builtin_fmaf(-rE, e, 1.0f), SE, -e), e);
                     I[u][r] = __builtin_fmaf(dtI, __builtin_fmaf(__builtin_fmaf(-rI, in, 1.0f), SI, -in), in);
+#if WC_INC2
+                    A[u][r].add(in * __builtin_fmaf(e, dtA, (float)(-a.rhoE * a.dtSim / a.tau_ip)));
+#else
                     const float tA = in * dtA;
                     A[u][r].add(__builtin_fmaf(e, tA, -rhoE * tA));
+#endif
                 }
                 continue;
             }
@@ -639,7 +668,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 const int n = 16 * (T0 + u) + 4 * g + r;
                 if (n < N) {
                     const size_t o = (size_t)b * N + n;
-                    a.E[o] = (double)E[u][r];
+                    a.E[o] = (double)(E[u][r] * (Real)kEinv);
                     a.I[o] = (double)I[u][r];
                     a.A[o] = A[u][r].get();
                 }
