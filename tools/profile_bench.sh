@@ -15,6 +15,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o p -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o p -- python3 bench.py $ARGS > $OUT/write.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VALU_TRANS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o p -- python3 bench.py $ARGS > $OUT/sq.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq2 -o p -- python3 bench.py $ARGS > $OUT/sq2.log 2>&1
 python3 - <<'PY'
 import json, sys
 sys.path.insert(0, "tools")
@@ -46,7 +47,36 @@ d = {"kernel": kf, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
              "HBM counters include Infinity-Cache traffic. A wave-step = one Euler step of one wave "
              "(16 simulations x 2 node tiles of 16; 3 waves per group of 16 simulations). mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / "
              "(GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)."}
+q2 = summary("gpurun_out/prof/sq2", "wc_sde_kernel")
+(_, v2), = q2.items()
+d["wave_cycle_split"] = {k: v2[k] / v2["SQ_WAVE_CYCLES"] for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")}
 json.dump(d, open("profiles/pmc_sde.json", "w"), indent=1)
+# the two signal kernels of the bench step: instruction counts per unit of work, issue and wait split
+sig = {"note": "rocprofv3 --pmc passes of the same bench run (tools/profile_bench.sh), averaged per dispatch. "
+               "Busy fractions: 4 x SQ_ACTIVE_INST_* quad-cycles / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); "
+               "wave_cycle_split: SQ_WAIT_ANY (parked on s_waitcnt/barrier), SQ_WAIT_INST_ANY (issue stall), "
+               "SQ_ACTIVE_INST_ANY (issuing), fractions of SQ_WAVE_CYCLES."}
+C = 20000 * 90
+for name, sub, units, per in (("bold_steady_copy", "bold_chunk_kernel<float, true, true, true>", C * 1000.0 / 64, "wave-sample"),
+                              ("welch", "welch_wave_kernel", float(C), "column-segment")):
+    a = summary("gpurun_out/prof/sq", sub)
+    b = summary("gpurun_out/prof/sq2", sub)
+    fe = summary("gpurun_out/prof/fetch", sub)
+    wr = summary("gpurun_out/prof/write", sub)
+    if not (a and b and fe and wr):
+        continue
+    (ka, va), = a.items(); (_, vb), = b.items(); (_, vf2), = fe.items(); (_, vw2), = wr.items()
+    act = va["GRBM_GUI_ACTIVE"] / 8 * simds
+    sig[name] = {"kernel": ka, "unit": per,
+                 "valu_insts_per_unit": va["SQ_INSTS_VALU"] / units,
+                 "lds_insts_per_unit": vb["SQ_INSTS_LDS"] / units,
+                 "valu_issue_busy_frac": 4 * va["SQ_ACTIVE_INST_VALU"] / act,
+                 "lds_bank_conflict_frac": vb["SQ_LDS_BANK_CONFLICT"] / max(1.0, vb["SQ_LDS_IDX_ACTIVE"]),
+                 "wave_cycle_split": {k: vb[k] / vb["SQ_WAVE_CYCLES"] for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")},
+                 "hbm_bytes_per_dispatch": 2 * vf2["FETCH_SIZE"] * 1024.0 + vw2["WRITE_SIZE"] * 1024.0,
+                 "dispatches": va["dispatches"]}
+json.dump(sig, open("profiles/pmc_signal.json", "w"), indent=1)
+json.dump(sig, open("gpurun_out/prof/pmc_signal.json", "w"), indent=1)
 json.dump(d, open("gpurun_out/prof/pmc_sde.json", "w"), indent=1)  # gpurun merges gpurun_out/ back only
 print(json.dumps(d))
 PY
