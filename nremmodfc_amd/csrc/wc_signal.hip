@@ -122,13 +122,23 @@ struct BoldArgs {
     int alpha_3125;  // 1/alpha == 3.125: v^(1/alpha) = v^3 * v^(1/8) by square roots
 };
 
+// The (h, G) table is read-only inside wc_bold_chunk, and its row r is wave-uniform.  Read
+// through the constant address space it becomes scalar loads (lgkmcnt).  Through the state
+// pointer, which the kernel also stores to, it was a vector load issued a few instructions
+// before its use.  That load is the youngest in vmcnt, so each sample's wait for it also
+// waited for the next batch's prefetched E loads.
+typedef const __attribute__((address_space(4))) double* tab_ptr;
+__device__ __forceinline__ tab_ptr tab_row(const double* st, const BoldLayout& L, int64_t r) {
+    return (tab_ptr)(st + L.tab) + 5 * r;
+}
+
 // forward output y of data sample k: accumulate the block's zero-state backward
 // summaries; at the block's last sample store them (block m = k / dec)
 // (r, m) = (k % dec, k / dec), passed in by the caller's running counters
 __device__ __forceinline__ void emit_rm(const BoldArgs& a, const BoldLayout& L, double* st, int64_t c, int64_t k,
                                         int64_t r, int64_t m, double y, double acc[5]) {
     const int64_t dec = a.cfg.dec;
-    const double* tab = st + L.tab + 5 * r;  // wave-uniform address: scalar loads
+    const tab_ptr tab = tab_row(st, L, r);  // wave-uniform row: scalar loads
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[j] += tab[j] * y;
     if (r == dec - 1 || k == a.n - 1) {
@@ -144,7 +154,7 @@ __device__ __forceinline__ void emit(const BoldArgs& a, const BoldLayout& L, dou
                                      double y, double acc[5]) {
     const int64_t dec = a.cfg.dec;
     const int64_t r = k % dec;
-    const double* tab = st + L.tab + 5 * r;  // wave-uniform address: scalar loads
+    const tab_ptr tab = tab_row(st, L, r);  // wave-uniform row: scalar loads
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[j] += tab[j] * y;
     if (r == dec - 1 || k == a.n - 1) {
@@ -324,7 +334,7 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? 3 :
     auto steady = [&](double x, int64_t r, int64_t m) {  // r, m: (block position, block) of the sample
         const double bold = balloon(x);
         const double y = BP ? iir_step_bp(zf, bold, b, fa) : iir_step(zf, bold, b, fa);
-        const double* tab = st + L.tab + 5 * r;  // wave-uniform address: scalar loads
+        const tab_ptr tab = tab_row(st, L, r);  // wave-uniform row: scalar loads
 #pragma unroll
         for (int j = 0; j < 5; ++j) acc[j] += tab[j] * y;
         if (r == a.cfg.dec - 1) {

@@ -400,11 +400,22 @@ __device__ __forceinline__ void wstage(f2* z, const f2* Ts, int lane) {
         for (int r = 0; r < RAD; ++r) u[q][r] = ldsr(z + i + r * R::S);
     }
     wave_sync();
+    // twiddles one row ahead: the volatile LDS reads are scheduling barriers, so a row's
+    // reads issued right before its own products were each waited on (one exposed LDS
+    // round trip per twiddle); issuing row q+1's reads before row q's products keeps
+    // them in flight behind that work
+    f2 tw[2][RAD - 1];
+#pragma unroll
+    for (int r = 1; r < RAD; ++r) tw[0][r - 1] = ldsr(Ts + TB + R::idx(lane, 0) % P + (r - 1) * P);
 #pragma unroll
     for (int q = 0; q < R::NB; ++q) {
-        const f2* tp = Ts + TB + R::idx(lane, q) % P;
+        if (q + 1 < R::NB) {
 #pragma unroll
-        for (int r = 1; r < RAD; ++r) u[q][r] = cmulv(u[q][r], ldsr(tp + (r - 1) * P));
+            for (int r = 1; r < RAD; ++r)
+                tw[(q + 1) & 1][r - 1] = ldsr(Ts + TB + R::idx(lane, q + 1) % P + (r - 1) * P);
+        }
+#pragma unroll
+        for (int r = 1; r < RAD; ++r) u[q][r] = cmulv(u[q][r], tw[q & 1][r - 1]);
     }
     write_rows<RAD, P>(z, u, lane);
     wave_sync();
@@ -458,12 +469,21 @@ __device__ __forceinline__ void wstage_last_unpack(const f2* z, const f2* Ts, co
 #pragma unroll
         for (int r = 0; r < 16; ++r) u[q][r] = ldsr(z + rows[q] + 125 * r);
     wave_sync();  // (the next column's stage 1 overwrites z)
+    // twiddle reads batched ahead of the work that needs them (see wstage): row 0's before
+    // its products, row 1's before row 0's DFT, the unpack's before row 1's DFT
+    f2 tw[2][15], tu[16];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int r = 1; r < 16; ++r) tw[0][r - 1] = ldsr(Ts + kTb4 + (r - 1) * 125 + rows[0]);
 #pragma unroll
-        for (int r = 1; r < 16; ++r) u[q][r] = cmulv(u[q][r], ldsr(Ts + kTb4 + (r - 1) * 125 + rows[q]));
-        dft16(u[q]);
-    }
+    for (int r = 1; r < 16; ++r) u[0][r] = cmulv(u[0][r], tw[0][r - 1]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) tw[1][r - 1] = ldsr(Ts + kTb4 + (r - 1) * 125 + rows[1]);
+    dft16(u[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) u[1][r] = cmulv(u[1][r], tw[1][r - 1]);
+#pragma unroll
+    for (int s2i = 0; s2i < 16; ++s2i) tu[s2i] = ldsr(Tu + m + 125 * s2i);
+    dft16(u[1]);
 #pragma unroll
     for (int s2i = 0; s2i < 16; ++s2i) {
         const f2 Zk = u[0][s2i];
@@ -471,7 +491,7 @@ __device__ __forceinline__ void wstage_last_unpack(const f2* z, const f2* Ts, co
         f2 sv, dv;
         asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
         asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
-        const f2 pv = cmulv(dv, ldsr(Tu + m + 125 * s2i));
+        const f2 pv = cmulv(dv, tu[s2i]);
         const f2 xa = add_mi(sv, pv), xb = sub_mi(sv, pv);
         acc[s2i][0] = fmaf(xa.x, xa.x, fmaf(xa.y, xa.y, acc[s2i][0]));
         acc[s2i][1] = fmaf(xb.x, xb.x, fmaf(xb.y, xb.y, acc[s2i][1]));
