@@ -214,7 +214,12 @@ enum : int {
     V_ILV = 2048,     // ... interleaved with them (sched_group_barrier: 1 MFMA, 6 VALU)
     V_ILV2 = 4096,    // ... interleaved with them (1 MFMA, 2 VALU: the free half of a 16x16x32 gap)
     V_SCALAR = 8192,  // ablation: the fp32 fast update one cell per instruction (round-2 form)
+    V_MIX = 16384,    // NT = 6 over NW = 4 waves per group, two waves with 2 tiles and two with 1,
+                      // the pattern rotated per group so the SIMDs of a 3-group workgroup carry
+                      // 5/4/5/4 tiles instead of 6/4/4/4 (3 waves of 2 tiles)
 };
+
+constexpr bool kFragRegs_(int var) { return (var & V_FRAG_REGS) != 0; }
 
 // SG > 1: one workgroup holds SG groups of 16 simulations (SG x NW waves) that
 // share ONE LDS copy of the connectome image; each group has its own E exchange.
@@ -222,8 +227,9 @@ template <typename Real, int NT, int NW, int VAR, int MINW, int SG = 1>
 __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs a) {
     typedef typename Tr<Real>::acc_t acc_t;
     typedef __attribute__((ext_vector_type(4))) Real real4;
-    static_assert(NT % NW == 0, "NW must divide NT");
-    constexpr int OT = NT / NW;
+    constexpr bool kMix = (VAR & V_MIX) != 0;
+    static_assert(kMix ? (NT == 6 && NW == 4) : NT % NW == 0, "NW must divide NT");
+    constexpr int OT = kMix ? 2 : NT / NW;  // tile slots per wave
     constexpr bool kHf = (VAR & V_F16X3) != 0;
     constexpr int kTerms = (VAR & V_BF16X6) ? 6 : (VAR & V_BF16X3) ? 3 : kHf ? 3 : 0;
     constexpr bool kBf = kTerms > 0;  // 16-bit split coupling (bf16 or fp16 parts)
@@ -263,7 +269,19 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     const bool live = b < a.B;
     const int bb = live ? b : a.B - 1;  // tail lanes mirror the last sim, never store
     const int N = a.N;
-    const int T0 = NW == 1 ? 0 : w * OT;
+    // this wave's tiles T0 .. T0 + nt - 1 (nt = OT except in V_MIX); a slot u >= nt maps to the
+    // dead tile NT, whose nodes (>= 96 >= N) every n < N test skips
+    int T0 = NW == 1 ? 0 : w * OT, nt = OT;
+    if constexpr (kMix) {
+        static_assert(!kFragRegs_(VAR) && (VAR & V_ZFIRST) == 0, "V_MIX: LDS fragments, plain schedule");
+        const int rot = grp & 3;
+        auto cnt = [&](int v) { return ((v + 4 - rot) & 3) < 2 ? 2 : 1; };  // (2, 2, 1, 1) rotated
+        nt = cnt(w);
+        T0 = 0;
+        for (int v = 0; v < w; ++v) T0 += cnt(v);
+    }
+    auto TL = [&](int u) { return !kMix || u < nt ? T0 + u : NT; };
+    auto owned = [&](int u) { return !kMix || u < nt; };  // (wave-uniform)
 
     // ---- A operand: this wave's rows, in registers or the whole image in LDS ----
     constexpr bool kRegBf = kFragRegs && kBf, kRegN = kFragRegs && !kBf;
@@ -278,12 +296,12 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
 #pragma unroll
-                    for (int p = 0; p < NP; ++p) F16[u][c][p] = g16[(((T0 + u) * NC + c) * PS + p) * 64 + lane];
+                    for (int p = 0; p < NP; ++p) F16[u][c][p] = g16[((TL(u) * NC + c) * PS + p) * 64 + lane];
         } else if constexpr (kRegN) {
 #pragma unroll
             for (int u = 0; u < OT; ++u)
 #pragma unroll
-                for (int t = 0; t < NT; ++t) FN[u][t] = gn[((T0 + u) * NT + t) * 64 + lane];
+                for (int t = 0; t < NT; ++t) FN[u][t] = gn[(TL(u) * NT + t) * 64 + lane];
         } else if constexpr (kBf) {
             bf16x8* l16 = reinterpret_cast<bf16x8*>(smem);
             for (int i = threadIdx.x; i < kFragUnits * 64; i += blockDim.x) l16[i] = g16[i];
@@ -306,7 +324,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     for (int u = 0; u < OT; ++u)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int n = 16 * (T0 + u) + 4 * g + r;
+            const int n = 16 * TL(u) + 4 * g + r;
             const bool ok = n < N;
             const size_t o = (size_t)bb * N + (ok ? n : 0);
             E[u][r] = ok ? (Real)a.E[o] * (Real)kEsc : (Real)0;
@@ -352,7 +370,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 bf16x4* x4 = reinterpret_cast<bf16x4*>(xb16 + buf * NC * PS * 64);
 #pragma unroll
                 for (int u = 0; u < OT; ++u) {
-                    const int t = T0 + u;  // chunk t/2, half t&1 (runtime: address arithmetic only)
+                    if (!owned(u)) continue;
+                    const int t = TL(u);  // chunk t/2, half t&1 (runtime: address arithmetic only)
                     bf16x4 hmo[3];
                     if constexpr (kHf) split2h<kEs>(E[u], reinterpret_cast<f16x4&>(hmo[0]), reinterpret_cast<f16x4&>(hmo[1]));
                     else split3(E[u], hmo[0], hmo[1], hmo[2]);
@@ -362,7 +381,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             } else {
                 real4* xb = xbn + buf * NT * 64;
 #pragma unroll
-                for (int u = 0; u < OT; ++u) xb[(T0 + u) * 64 + lane] = real4{E[u][0], E[u][1], E[u][2], E[u][3]};
+                for (int u = 0; u < OT; ++u) xb[TL(u) * 64 + lane] = real4{E[u][0], E[u][1], E[u][2], E[u][3]};
             }
             __syncthreads();  // no LDS-DMA in flight: lgkmcnt(0) + s_barrier
         }
@@ -410,7 +429,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                             for (int u = 0; u < OT; ++u)
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
-                                    const int n = 16 * (T0 + u) + 4 * g + r;
+                                    const int n = 16 * TL(u) + 4 * g + r;
                                     if (n < N) {
                                         Real* dst = static_cast<Real*>(a.recE) + ((size_t)bb * N + n) * a.rec_ld +
                                                     (rec_row - (RB - 1));
@@ -439,7 +458,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     for (int u = 0; u < OT; ++u)
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            const int n = 16 * (T0 + u) + 4 * g + r;
+                            const int n = 16 * TL(u) + 4 * g + r;
                             if (n < N) {
                                 const size_t cc = (size_t)bb * N + n;
                                 const size_t o = a.rec_ld ? cc * a.rec_ld + rec_row : (size_t)rec_row * BN + cc;
@@ -466,7 +485,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         float zz[kZFirst ? OT : 1][4];
         if constexpr (kZFirst) {
 #pragma unroll
-            for (int u = 0; u < OT; ++u) quad_normals_raw(gstep, (uint32_t)(4 * (T0 + u) + g), key, zz[u]);
+            for (int u = 0; u < OT; ++u) quad_normals_raw(gstep, (uint32_t)(4 * TL(u) + g), key, zz[u]);
         }
         if constexpr (kMfma && kBf) {
             const bf16x8* l16 = reinterpret_cast<const bf16x8*>(smem);
@@ -481,11 +500,12 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 }
 #pragma unroll
                 for (int u = 0; u < OT; ++u) {
+                    if (!owned(u)) continue;
                     bf16x8 f[NP];
 #pragma unroll
                     for (int p = 0; p < NP; ++p) {
                         if constexpr (kFragRegs) f[p] = F16[u][c][p];
-                        else f[p] = l16[(((T0 + u) * NC + c) * PS + p) * 64 + fl];
+                        else f[p] = l16[((TL(u) * NC + c) * PS + p) * 64 + fl];
                     }
                     if constexpr (kHf) {  // small terms first: 2^-11 (lo.hi, hi.lo), 1 (hi.hi)
                         typedef f16x8 h8;
@@ -523,7 +543,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 for (int u = 0; u < OT; ++u) {
                     if constexpr (!kFragRegs && sizeof(Real) == 8)
                         if ((u & 1) == 0) __builtin_amdgcn_sched_barrier(0);  // bound fp64 read look-ahead
-                    const real4 f = kFragRegs ? FN[u][t] : ln[((T0 + u) * NT + t) * 64 + fl];
+                    const real4 f = kFragRegs ? FN[u][t] : ln[(TL(u) * NT + t) * 64 + fl];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) acc[u] = Tr<Real>::mfma(f[r], xe[r], acc[u]);
                 }
@@ -543,6 +563,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         // ---- elementwise update (wc:77-83), noise drawn inside the E sigmoid ----
 #pragma unroll
         for (int u = 0; u < OT; ++u) {
+            if (!owned(u)) continue;
             if constexpr (sizeof(Real) == 8) __builtin_amdgcn_sched_barrier(0);  // fp64: bound live ranges
             Real z[4] = {0, 0, 0, 0};
             if constexpr (kFast && kPk) {
@@ -551,7 +572,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     zp[0] = f2v{zz[u][0], zz[u][1]};
                     zp[1] = f2v{zz[u][2], zz[u][3]};
                 } else if constexpr (kRng) {
-                    quad_normals_pk(gstep, (uint32_t)(4 * (T0 + u) + g), key, zp);
+                    quad_normals_pk(gstep, (uint32_t)(4 * TL(u) + g), key, zp);
                 }
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -576,7 +597,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                     for (int r = 0; r < 4; ++r) z[r] = zz[u][r];
                 } else if constexpr (kRng) {
-                    quad_normals_raw(gstep, (uint32_t)(4 * (T0 + u) + g), key, z);
+                    quad_normals_raw(gstep, (uint32_t)(4 * TL(u) + g), key, z);
                 }
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -604,7 +625,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 }
                 continue;
             }
-            if constexpr (kRng) quad_normals(gstep, (uint32_t)(4 * (T0 + u) + g), key, z);
+            if constexpr (kRng) quad_normals(gstep, (uint32_t)(4 * TL(u) + g), key, z);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const Real e = E[u][r], in = I[u][r];
@@ -614,7 +635,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     gc = Gc[u][r];
                     sl = Sl[u][r];
                 } else {
-                    const int n = 16 * (T0 + u) + 4 * g + r;
+                    const int n = 16 * TL(u) + 4 * g + r;
                     const size_t o = (size_t)bb * N + (n < N ? n : 0);
                     gc = n < N ? (Real)a.G[o] : (Real)0;
                     sl = n < N ? Tr<Real>::slope(a.sigmaE[o]) : (Real)0;
@@ -649,7 +670,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             for (int u = 0; u < OT; ++u)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int n = 16 * (T0 + u) + 4 * g + r;
+                    const int n = 16 * TL(u) + 4 * g + r;
                     if (n < N) {
                         Real* dst = static_cast<Real*>(a.recE) + ((size_t)bb * N + n) * a.rec_ld + (rec_row - m);
 #pragma unroll
@@ -665,7 +686,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         for (int u = 0; u < OT; ++u)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int n = 16 * (T0 + u) + 4 * g + r;
+                const int n = 16 * TL(u) + 4 * g + r;
                 if (n < N) {
                     const size_t o = (size_t)b * N + n;
                     a.E[o] = (double)(E[u][r] * (Real)kEinv);
@@ -768,7 +789,13 @@ int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) 
                       ((uintptr_t)ka.recE & 7) == 0;
     constexpr int V2 = V | V_REC2;
     switch (std::min(5, (groups + cus - 1) / cus)) {
+#ifndef WC_NO_MIX
+        // three groups per CU: four waves per group with (2, 2, 1, 1) tiles rotated per group (V_MIX)
+        case 3: return rec2 ? launch_v<float, 6, 4, V2 | V_MIX, 1, 3>(ka, sc, ws, st)
+                            : launch_v<float, 6, 4, V | V_MIX, 1, 3>(ka, sc, ws, st);
+#else
         case 3: return rec2 ? launch_v<float, 6, 3, V2, 1, 3>(ka, sc, ws, st) : launch_v<float, 6, 3, V, 1, 3>(ka, sc, ws, st);
+#endif
         case 4: return rec2 ? launch_v<float, 6, 3, V2, 1, 4>(ka, sc, ws, st) : launch_v<float, 6, 3, V, 1, 4>(ka, sc, ws, st);
         default: return rec2 ? launch_v<float, 6, 3, V2, 1, 5>(ka, sc, ws, st) : launch_v<float, 6, 3, V, 1, 5>(ka, sc, ws, st);
     }
