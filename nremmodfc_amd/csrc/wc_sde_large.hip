@@ -632,7 +632,12 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
 constexpr int kPN = 128, kPS = 80, kPT = kPS / 16;  // nodes, simulations, simulation tiles per workgroup
 constexpr int kPWaves = kPN / 16;                     // 8
 constexpr uint32_t kSpinLimit = 1u << 22;             // polls per wait before giving up (~seconds)
-constexpr int kPRes = 8;  // K chunks of the connectome tile kept in LDS (128 KB of the 512 KB streamed per step)
+#ifndef WC_PPAIR
+#define WC_PPAIR 1
+#endif
+// K chunks of the connectome tile kept in LDS (112 KB of the 512 KB streamed per step; 8 chunks
+// = 128 KB before the image stages were paired, WC_PPAIR)
+constexpr int kPRes = WC_PPAIR ? 7 : 8;
 
 struct PGeo {
     int B, N, Np, Bp, MT, NC, SBp, NBp;
@@ -719,7 +724,8 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
     // [stage][part x sim tile][lane] B (2 stages); per-simulation G, slope and keys.  The state and
     // the A fragments live in registers (~215 VGPRs: one workgroup per CU).
-    __shared__ f16x8 ldsB[2][kParts * kPT][64];
+    // image stages: WC_PPAIR stages the two chunks of a pair behind one barrier (16 per step, not 32)
+    __shared__ f16x8 ldsB[2][WC_PPAIR ? 2 : 1][kParts * kPT][64];
     __shared__ f16x8 ldsA[kPRes][kPWaves][kParts][64];  // the first kPRes K chunks of the connectome rows, resident
     __shared__ float2 ldsGS[kPS];
     __shared__ uint64_t ldsK[kPS];
@@ -846,17 +852,12 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         rb[slot][0] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 16));
         if (tid < 128) rb[slot][1] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo + 512 * 16, 0, 16));
     };
-    auto do_chunk = [&](int c, int slot, int buf, f4 (&acc)[kPT]) {
-        reinterpret_cast<u4*>(&ldsB[slot][0][0])[tid] = rb[slot][0];
-        if (tid < 128) reinterpret_cast<u4*>(&ldsB[slot][0][0])[512 + tid] = rb[slot][1];
-        __syncthreads();  // stage `slot` was last read at chunk c - 2, before the previous barrier
-        // (each wave reads only its own ldsA slice, written by itself before the step loop)
-        const f16x8 a0 = c < res ? ldsA[c][w][0][lane] : fa[slot][0];
-        const f16x8 a1 = c < res ? ldsA[c][w][1][lane] : fa[slot][1];
-        if (c + 2 < g.NC) load_chunk(c + 2, slot, buf);
+    // chunk c's MFMAs from image stage `st` (each wave reads only its own ldsA slice, written by
+    // itself before the step loop)
+    auto mfma_chunk = [&](int c, f16x8 a0, f16x8 a1, const f16x8 (*stg)[64], f4 (&acc)[kPT]) {
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
-            const f16x8 fb0 = ldsB[slot][t][lane], fb1 = ldsB[slot][kPT + t][lane];
+            const f16x8 fb0 = stg[t][lane], fb1 = stg[kPT + t][lane];
             if (DIAG == 1) {
                 acc[t][0] += (float)fb0[0] + (float)a0[0] + (float)fb1[1] + (float)a1[1];
                 continue;
@@ -866,6 +867,38 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb1, acc[t], 0, 0, 0);
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb0, acc[t], 0, 0, 0);
         }
+    };
+    // WC_PPAIR: chunks c, c + 1 (a pair) staged together into pair stage (c / 2) & 1 behind ONE
+    // barrier; that stage was last read two pairs ago, before the previous pair's barrier.  The
+    // pair's A operands are taken before the next pair's loads overwrite fa.
+    auto do_pair = [&](int c, int buf, f4 (&acc)[kPT]) {
+        const int ps = (c >> 1) & 1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            reinterpret_cast<u4*>(&ldsB[ps][h][0][0])[tid] = rb[h][0];
+            if (tid < 128) reinterpret_cast<u4*>(&ldsB[ps][h][0][0])[512 + tid] = rb[h][1];
+        }
+        __syncthreads();
+        const f16x8 a00 = c < res ? ldsA[c][w][0][lane] : fa[0][0];
+        const f16x8 a01 = c < res ? ldsA[c][w][1][lane] : fa[0][1];
+        const f16x8 a10 = c + 1 < res ? ldsA[c + 1][w][0][lane] : fa[1][0];
+        const f16x8 a11 = c + 1 < res ? ldsA[c + 1][w][1][lane] : fa[1][1];
+        if (c + 2 < g.NC) {
+            load_chunk(c + 2, 0, buf);
+            load_chunk(c + 3, 1, buf);
+        }
+        mfma_chunk(c, a00, a01, ldsB[ps][0], acc);
+        mfma_chunk(c + 1, a10, a11, ldsB[ps][1], acc);
+    };
+    auto do_chunk = [&](int c, int slot, int buf, f4 (&acc)[kPT]) {
+        reinterpret_cast<u4*>(&ldsB[slot][0][0][0])[tid] = rb[slot][0];
+        if (tid < 128) reinterpret_cast<u4*>(&ldsB[slot][0][0][0])[512 + tid] = rb[slot][1];
+        __syncthreads();  // stage `slot` was last read at chunk c - 2, before the previous barrier
+        // (each wave reads only its own ldsA slice, written by itself before the step loop)
+        const f16x8 a0 = c < res ? ldsA[c][w][0][lane] : fa[slot][0];
+        const f16x8 a1 = c < res ? ldsA[c][w][1][lane] : fa[slot][1];
+        if (c + 2 < g.NC) load_chunk(c + 2, slot, buf);
+        mfma_chunk(c, a0, a1, ldsB[slot][0], acc);
     };
     for (int64_t s = 0; s < a.nsteps && alive; ++s) {
         const int buf = (int)(s & 1);
@@ -880,8 +913,12 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         load_chunk(0, 0, buf);
         load_chunk(1, 1, buf);
         for (int c = 0; c < g.NC; c += 2) {  // NC is a multiple of 4 (nodes padded to 128)
-            do_chunk(c, 0, buf, acc);
-            do_chunk(c + 1, 1, buf, acc);
+            if (WC_PPAIR) {
+                do_pair(c, buf, acc);
+            } else {
+                do_chunk(c, 0, buf, acc);
+                do_chunk(c + 1, 1, buf, acc);
+            }
         }
         // ---- epilogue: step_kernel's update on the D fragments (the state in registers) ----
         const uint64_t gstep = (uint64_t)(a.step0 + s);
