@@ -376,7 +376,8 @@ __device__ __forceinline__ void wstage1(f2* z, f2 (&x)[7][5], const f2* __restri
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
             part += R::own(lane, q) ? x[q][r].x + x[q][r].y : 0.f;
-            hw[q][r] = hann[i + r * R::S];  // (w(2m), w(2m+1))
+            // (w(2m), w(2m+1)); unsigned byte offset: the saddr form of the load
+            hw[q][r] = *reinterpret_cast<const f2*>(reinterpret_cast<const char*>(hann) + (unsigned)(i + r * R::S) * 8u);
         }
     }
     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
@@ -500,7 +501,9 @@ __device__ __forceinline__ void wstage_last_unpack(const f2* z, const f2* Ts, co
 
 __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const WelchArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int wg = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // (the wave index through readfirstlane: the column base is then scalar and every load the
+    // saddr form, an SGPR base plus a 32-bit lane offset, instead of a 64-bit VGPR address each)
+    const int wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int w = wg & (kWv - 1);                         // column slot within the simulation
     const int b = blockIdx.x * kSimsWg + wg / kWv;        // this wave's simulation
     const int ncol = b < a.B ? a.N : 0;
@@ -514,8 +517,9 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
 #pragma unroll
     for (int s2i = 0; s2i < 16; ++s2i) acc[s2i][0] = acc[s2i][1] = 0.f;
     // the ring is circular per column: sample seg0 + t sits at (seg0 + t) mod L, L = slot * nslots
+    // (byte offsets in 32 bits: the host admits ld < INT32_MAX / 2 - 8192, so 4 (L + 4000) < 2^32)
     const unsigned L = (unsigned)(a.slot * a.nslots);
-    const unsigned base = (unsigned)(a.seg0 % L);
+    const unsigned baseB = (unsigned)(a.seg0 % L) * 4u, LB = L * 4u;
     // stage-1 inputs come straight from HBM into registers, in the butterfly layout
     // (x[q][r] = packed point i + 400 r, i = lane + 64 q); the next column is fetched
     // while the current one is transformed (branch-free: the clamped lanes of row 6
@@ -529,9 +533,9 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         _Pragma("unroll") for (int q = Q0; q < Q1; ++q) {                                      \
             const int i_ = Rows<5, 1>::idx(LN, q);                                            \
             _Pragma("unroll") for (int r = 0; r < 5; ++r) {                                    \
-                unsigned o_ = base + 2 * (i_ + 400 * r);                                       \
-                o_ = min(o_, o_ - L);                                                          \
-                x[q][r] = *reinterpret_cast<const f2*>(col_ + o_);                             \
+                unsigned o_ = baseB + 8u * (unsigned)(i_ + 400 * r);                           \
+                o_ = min(o_, o_ - LB);                                                         \
+                x[q][r] = *reinterpret_cast<const f2*>(reinterpret_cast<const char*>(col_) + o_); \
             }                                                                                  \
         }                                                                                      \
     }
@@ -654,7 +658,7 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
         if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
         hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
     } else {
-        if (ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 && ld < INT32_MAX / 2) {
+        if (ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 && ld < INT32_MAX / 2 - 8192) {
             hipError_t ea = hipFuncSetAttribute((const void*)welch_wave_kernel,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWelchLds);
             if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
