@@ -452,6 +452,14 @@ __device__ __forceinline__ void dft16(f2 (&u)[16]) {
     }
 }
 
+// acc + v * v as one v_fma_f32 (written out: the compiler pairs the two bins' accumulators into
+// v_pk_fma_f32 and transposes their operands with three v_mov per pair, 5 VALU for 4 fmas)
+__device__ __forceinline__ float sq_acc(float v, float acc) {
+    float r;
+    asm("v_fma_f32 %0, %1, %1, %2" : "=v"(r) : "v"(v), "v"(acc));
+    return r;
+}
+
 // Last stage (radix 16, P = 125) fused with the real-FFT unpack, all in registers.
 // Butterfly i produces Z_{i + 125 s}, s = 0..15; bin k pairs Z_k with Z_{2000-k}, and
 // Z_{2000 - (i + 125 s)} is slot 15 - s of butterfly 125 - i.  Row 0 of a lane holds
@@ -494,8 +502,8 @@ __device__ __forceinline__ void wstage_last_unpack(const f2* z, const f2* Ts, co
         asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
         const f2 pv = cmulv(dv, tu[s2i]);
         const f2 xa = add_mi(sv, pv), xb = sub_mi(sv, pv);
-        acc[s2i][0] = fmaf(xa.x, xa.x, fmaf(xa.y, xa.y, acc[s2i][0]));
-        acc[s2i][1] = fmaf(xb.x, xb.x, fmaf(xb.y, xb.y, acc[s2i][1]));
+        acc[s2i][0] = sq_acc(xa.x, sq_acc(xa.y, acc[s2i][0]));
+        acc[s2i][1] = sq_acc(xb.x, sq_acc(xb.y, acc[s2i][1]));
     }
 }
 

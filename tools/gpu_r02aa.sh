@@ -1,5 +1,5 @@
 #!/bin/bash
-# Welch loads in the saddr form (scalar column base, 32-bit byte offsets): bit-compare + timing against HEAD, the
+# Welch kernel change vs the HEAD build of wc_welch.hip (tools/dbg/libwcsde_welchhead.so): bit-compare + timing, the
 # signal GPU tests, and the bench line of the new build
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
