@@ -876,6 +876,11 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 36: return launch_v<float, 6, 2, V_F16X3 | V_FRAG_REGS | K | V_ZFIRST>(ka, sc, ws, st);
         // 37: the C3 product configuration (SG = 5, paired records) with the round-2 one-cell-per-instruction update
         case 37: return launch_v<float, 6, 3, V_F16X3 | K | V_REC2 | V_SCALAR, 1, 5>(ka, sc, ws, st);
+        // the C3 product kernel (launch_f32_nt6's SG = 5 case, time-major records) and its ablations:
+        // noise off, coupling MFMAs off
+        case 38: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A, 1, 5>(ka, sc, ws, st);
+        case 39: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_NO_RNG, 1, 5>(ka, sc, ws, st);
+        case 40: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_NO_MFMA, 1, 5>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
@@ -947,9 +952,11 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
                       int64_t nsteps, double tau_ip, int64_t rec_every, void* recE, void* workspace,
                       size_t ws_bytes, void* stream) {
     KArgs ka;
-    // variants 20..22 record node-major into a dense [B*N][ld] buffer, ld = n_rec rounded up to 4
+    // variants 20..37 record node-major into a dense [B*N][ld] buffer, ld = n_rec rounded up to 4
+    // (38..40, the product's ablations, record time-major as the C3 pipeline does)
     const int64_t n_rec = rec_every > 0 ? (nsteps + rec_every - 1) / rec_every : 0;
-    const int64_t ld = (variant >= 20 && variant < 100 && rec_every > 0) ? (n_rec + 3) & ~int64_t(3) : 0;
+    const bool nm = variant >= 20 && variant < 38;
+    const int64_t ld = (nm && rec_every > 0) ? (n_rec + 3) & ~int64_t(3) : 0;
     int rc = make_args(ka, p, WC_F32, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, ld,
                        recE, nullptr, nullptr, workspace, ws_bytes);
     if (rc != WC_OK || nsteps == 0) return rc;

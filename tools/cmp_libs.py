@@ -8,7 +8,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-CASES = [(90, 20000, True), (90, 10000, False), (90, 2500, True), (90, 60, False), (60, 700, False), (30, 100, False)]
+CASES = [(90, 20000, True), (90, 20000, False), (90, 10000, False), (90, 2500, True), (90, 60, False), (60, 700, False), (30, 100, False)]
 
 
 def save(out):

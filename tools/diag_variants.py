@@ -57,7 +57,7 @@ def main():
     for v in variants:
         bt = Batch(sc, sG, sS, sk, p, precision="f32")
         diag(bt, v, 300, 0.05)
-        if 20 <= v < 100:  # node-major [B*N][32] records
+        if 20 <= v < 38:  # node-major [B*N][32] records
             rec = torch.empty((37 * 90, 32), dtype=torch.float32, device="cuda")
             diag(bt, v, 600, 2.0, 20, rec)
             got = rec[:, :30].reshape(37, 90, 30).permute(0, 2, 1)
@@ -80,7 +80,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             rec_every = int(os.environ.get("DIAG_REC", "20"))
-            diag(bt, v, steps, 2.0, rec_every, (recn if 20 <= v < 100 else rec) if rec_every else None)
+            diag(bt, v, steps, 2.0, rec_every, (recn if 20 <= v < 38 else rec) if rec_every else None)
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1))
