@@ -252,3 +252,30 @@ def test_f32_gate_detects_coupling_error(cuda, sc90, rel):
     d = np.abs(rec.double().cpu().numpy().transpose(1, 0, 2) - o)
     mx, rms = observed(d, f"gate-coupling-{rel:+.1e}")
     assert mx > 2e-6 or rms > 3e-7, (mx, rms)
+
+
+@pytest.mark.parametrize("name", ["homo", "maps"])
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_matches_reference_run_replay(cuda, sc90, prec, name):
+    """The device integrator against the REFERENCE's own run() (netwWilsonCowanPlastic.py:86-137
+    executed with numba decorators as identities and np.random.normal replaying the Philox
+    stream, tests/golden/make_ref_replay.py): E, I and a_ie at every recorded step of
+    100 + 100 + 2000 Euler steps.  fp64 <= 1e-9; fp32 at about 10x the observed deviation."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_replay.npz"))
+    n1, n2, n3 = (int(x) for x in d["steps"])
+    R = int(d["rec_every"])
+    gb = Batch(sc90, d[f"{name}_G"][None], d[f"{name}_sigmaE"][None], [int(d[f"{name}_key"])],
+               driver_params(), precision=prec)
+    gb.integrate(n1, 0.05)
+    gb.integrate(n2, 1.0)
+    recs = [torch.empty((n3 // R, 1, 90), dtype=gb.rec_dtype, device="cuda") for _ in range(3)]
+    gb.integrate(n3, 2.0, R, *recs)
+    torch.cuda.synchronize()
+    got = np.stack([r[:, 0].double().cpu().numpy() for r in recs], axis=1)  # [n_rec][3][N]
+    diff = np.abs(got - d[f"{name}_Y"])
+    mx, rms = observed(diff, f"ref-replay-{name}-{prec}")
+    if prec == "f64":
+        assert mx <= 1e-9, diff.max(axis=(0, 2))
+    else:
+        assert mx <= 1e-3 and rms <= 3e-5, (mx, rms)

@@ -11,7 +11,7 @@ fatal() { local rc=$1; [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; }
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -rA > $OUT/pytest_gpu.log 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
       echo "pytest gpu rc=$rc"; tail -25 $OUT/pytest_gpu.log
       if fatal $rc; then echo "STOP after tests"; exit $rc; fi ;;
     smoke)
