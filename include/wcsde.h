@@ -11,8 +11,10 @@
  * Conventions
  *  - every array argument is DEVICE memory owned by the caller (e.g. a
  *    torch.cuda tensor's data_ptr()), contiguous, batch-major unless stated;
- *  - no allocation, no host synchronisation inside a call: work is enqueued on
- *    `stream` (a hipStream_t, NULL = default stream) and the call returns;
+ *  - no allocation inside a call; work is enqueued on `stream` (a hipStream_t,
+ *    NULL = default stream) and the call returns without host synchronisation --
+ *    except wc_integrate's persistent N > 96 fp32 path, which synchronises `stream`
+ *    once per call to read its inter-workgroup hand-off error word (see there);
  *  - return 0 on success or a negative WC_E* code; wc_last_error() gives a
  *    thread-local message for the last failure on the calling thread;
  *  - reentrant: no global mutable state.
@@ -27,7 +29,7 @@
 extern "C" {
 #endif
 
-#define WCSDE_ABI_VERSION 4
+#define WCSDE_ABI_VERSION 5
 
 /* Noise stream (the reference's numba RNG is seeded from os.urandom and never
  * reproducible; the build defines its own): Philox4x32-10 with
@@ -101,8 +103,18 @@ size_t wc_workspace_size(int B, int N, int precision);
  *            compensated fp32 pair;
  *            WC_F64: everything fp64 (the parity mode).
  *  N <= 96   one launch integrates all nsteps with the state in registers;
- *  N > 96    one GEMM-shaped launch per Euler step (wc_sde_large.hip), the
- *            state in the workspace between steps; same noise stream.
+ *  N > 96    fp32, nsteps > 1 (the default): ONE persistent cooperative launch
+ *            (wc_sde_large.hip persist_kernel) -- one workgroup per CU owns 128
+ *            nodes x 80 simulations with their state in registers for all nsteps;
+ *            the 8 node blocks of a simulation block exchange the E operand image
+ *            through the workspace every step (bounded waits).  If the grid cannot
+ *            be made co-resident (cooperative launch refused: too many blocks, or
+ *            the CUs are shared) or WCSDE_PERSISTENT=0, and for fp64: one
+ *            GEMM-shaped launch per Euler step (step_kernel), the state in the
+ *            workspace between steps.  Both give the same bits.  The persistent
+ *            path synchronises `stream` after its launch and returns WC_EHIP if an
+ *            inter-workgroup wait timed out (E, I, A are then NaN).  Same noise
+ *            stream on every path.
  */
 int wc_integrate(const wc_params* p, int precision, int B, int N,
                  const double* sc, const double* G, const double* sigmaE,
@@ -115,6 +127,15 @@ int wc_integrate(const wc_params* p, int precision, int B, int N,
  * (float or double per precision).  Test hook for the noise stream. */
 int wc_noise(int precision, int B, int N, const uint64_t* keys, int64_t step,
              void* out, void* stream);
+
+/* One evaluation of netwWilsonCowanPlastic.wilsonCowan(t, X, sigmaE, mu, tau_ip, G)
+ * (wc:77-83), fp64, for B simulations: X [B][3][N] rows (E, I, a_ie) -> out
+ * [B][3][N] = (dE/dt, dI/dt, da_ie/dt).  The noise of wc:80 is sqdtD times the
+ * normals of Philox step `step` of each key (the integrator's normals at that
+ * global step); p->mu is the call's mu.  G, sigmaE [B][N]; sc [N][N]. */
+int wc_rhs(const wc_params* p, int B, int N, const double* sc, const double* G,
+           const double* sigmaE, const uint64_t* keys, int64_t step, double tau_ip,
+           const double* X, double* out, void* stream);
 
 /* ------------------------------------------------------------------------
  * simBOLD (netwWilsonCowanPlastic.py:140-158), streamed.
@@ -159,6 +180,15 @@ int wc_bold_finish(const wc_bold_cfg* cfg, int64_t C, const double* state, doubl
  * by cyclic Jacobi in LDS, one workgroup per matrix. */
 int wc_hma(int B, int N, double* fc, double* hin, double* hse, double* hin_node, double* hse_node,
            int* clus_num, double* sv, void* stream);
+
+/* The same outputs for any N >= 3 (N > 96: the matrix does not fit the Jacobi's
+ * LDS) from the eigensystem of F = (max(FC,0) + max(FC,0)^T)/2 computed by the
+ * caller on the device: lam [B][N] eigenvalues (any order), vt [B][N][N] with row
+ * j the eigenvector of lam[j].  Ranks |lam| (stable, descending), walks the
+ * levels (HMA.py:62-101), Balance and nodal_measures as wc_hma.  N <= 6700
+ * (LDS label arrays). */
+int wc_hma_modes(int B, int N, const double* lam, const double* vt, double* hin, double* hse,
+                 double* hin_node, double* hse_node, int* clus_num, double* sv, void* stream);
 
 /* ------------------------------------------------------------------------
  * SC optimiser (optimize_SC_Hopf.py:47-104), SURVEY.md 8f rank 4.

@@ -10,8 +10,8 @@ negative part then its positive part; empty modules dropped).
 
 The per-matrix functions run on the host (numpy SVD), with the reference's call
 surface.  The sweep path uses integration_segregation_batch: the same quantities
-for a whole batch in one device launch (wc_hma, nremmodfc_amd/csrc/wc_hma.hip;
-SURVEY.md 8f rank 3).  Like the reference, every function clips the caller's FC
+for a whole batch on the device (wc_hma / wc_hma_modes, nremmodfc_amd/csrc/wc_hma.hip;
+SURVEY.md 8f rank 3), at any N.  Like the reference, every function clips the caller's FC
 in place (FC[FC < 0] = 0, HMA.py:55) -- run_many_seeds saves that clipped sFC.
 """
 import numpy as np
@@ -90,7 +90,9 @@ def integration_segregation(sFC):
 
 
 def integration_segregation_batch(sfcs, device="cuda"):
-    """integration_segregation for a batch [B][N][N] (N <= 96) in one device launch.
+    """integration_segregation for a batch [B][N][N] on the device: one wc_hma launch
+    (Jacobi in LDS) for N <= 96; for N > 96 the batched device eigensolver and one
+    wc_hma_modes launch (sigchain.hma).
 
     Returns one dict per matrix with the keys run_many_seeds.py:134-136 pickles;
     sFC is the clipped matrix (as the reference saves it).

@@ -65,6 +65,9 @@ _SIGNATURES = {
     "wc_corrcoef_workspace_size": (c_sz, [c_int, c_int, c_int]),
     "wc_corrcoef": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "wc_hma": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wc_hma_modes": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "wc_rhs": (c_int, [ctypes.POINTER(WCParamsC), c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp,
+                       c_vp]),
     "wc_hopf_workspace_size": (c_sz, [c_int, c_int]),
     "wc_hopf_integrate": (c_int, [ctypes.POINTER(WCHopfParamsC), c_int, c_int, c_vp, c_vp, c_vp, c_vp,
                                   c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),

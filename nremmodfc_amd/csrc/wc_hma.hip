@@ -237,6 +237,119 @@ __global__ void __launch_bounds__(kThreads) hma_kernel(int N, double* __restrict
         for (int m = tid; m < N; m += kThreads) sv_out[(size_t)blockIdx.x * N + m] = lam[rank[m]];
 }
 
+// ---- N > 96: the module / Balance / nodal stages from a given eigensystem ----
+// lam [N] eigenvalues and vt [N][N] (row j = eigenvector j) of F = (max(FC,0) + max(FC,0)^T)/2,
+// from a batched library eigensolver on the device (the matrix no longer fits LDS for the Jacobi
+// above).  Same ranking, levels and sums as hma_kernel; the eigenvector rows are read from
+// global memory (coalesced: one row per level).  Compaction of a level's 2C candidate labels is
+// a wave-wide ballot scan instead of a serial loop (C grows to N).
+__global__ void __launch_bounds__(kThreads) hma_modes_kernel(int N, const double* __restrict__ lam_in,
+                                                             const double* __restrict__ vt_all,
+                                                             double* __restrict__ hin, double* __restrict__ hse,
+                                                             double* __restrict__ hin_node,
+                                                             double* __restrict__ hse_node, int* __restrict__ clus_num,
+                                                             double* __restrict__ sv_out) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* lam = lds;                                // [N] |lambda|
+    double* hf = lam + N;                             // [N]
+    int* rank = reinterpret_cast<int*>(hf + N);       // [N]
+    int* lab = rank + N;                              // [N]
+    int* flag = lab + N;                              // [2N]
+    int* newid = flag + 2 * N;                        // [2N]
+    const int tid = threadIdx.x;
+    const size_t b = blockIdx.x;
+    const double* vt = vt_all + b * (size_t)N * N;
+    for (int i = tid; i < N; i += kThreads) lam[i] = fabs(lam_in[b * N + i]);
+    __syncthreads();
+    for (int i = tid; i < N; i += kThreads) {
+        const double li = lam[i];
+        int r = 0;
+        for (int j = 0; j < N; ++j) r += (lam[j] > li) || (lam[j] == li && j < i);
+        rank[r] = i;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        for (int k = tid; k < N; k += 64) lab[k] = 0;
+        int C = 1;
+        for (int m = 0; m <= N - 2; ++m) {
+            for (int j = tid; j < C; j += 64) flag[j] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int k = tid; k < N; k += 64) atomicAdd(&flag[lab[k]], 1);  // module sizes of level m
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double pm = 0.0;
+            for (int j = tid; j < C; j += 64) pm += fabs((double)flag[j] - (double)N / C);
+            for (int o = 32; o > 0; o >>= 1) pm += __shfl_xor(pm, o);
+            if (tid == 0) {
+                const double sm = lam[rank[m]];
+                hf[m] = sm * sm * C * (1.0 - (m < N - 2 ? pm / N : 0.0));  // HMA.py:141-147 (p[N-2] stays 0)
+                if (clus_num) clus_num[b * (N - 1) + m] = C;
+            }
+            if (m == N - 2) break;
+            const double* u = vt + (size_t)rank[m + 1] * N;
+            for (int j = tid; j < 2 * C; j += 64) flag[j] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int k = tid; k < N; k += 64) {
+                const int l = 2 * lab[k] + (u[k] >= 0.0 ? 1 : 0);  // HMA.py:78-82: u >= 0 vs u < 0
+                lab[k] = l;
+                flag[l] = 1;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int run = 0;  // exclusive scan of the non-empty flags: compact ids in candidate order
+            for (int base = 0; base < 2 * C; base += 64) {
+                const int j = base + tid;
+                const bool f = j < 2 * C && flag[j] != 0;
+                const uint64_t mask = __ballot(f);
+                if (j < 2 * C) newid[j] = run + __popcll(mask & ((1ull << tid) - 1ull));
+                run += __popcll(mask);
+            }
+            C = run;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int k = tid; k < N; k += 64) lab[k] = newid[lab[k]];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    __syncthreads();
+    const double N2 = (double)N * N;
+    if (tid < 64) {
+        double s = 0.0;
+        for (int m = 1 + tid; m <= N - 2; m += 64) s += hf[m];
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if (tid == 0) {
+            hin[b] = hf[0] / N2;
+            hse[b] = s / N2;
+        }
+    }
+    // nodal measures (HMA.py:193-201): row rank[m] of vt is u_m, read coalesced per level
+    for (int k0 = 0; k0 < N; k0 += kThreads) {
+        const int k = k0 + tid;
+        if (k >= N) break;
+        const double u0 = vt[(size_t)rank[0] * N + k];
+        hin_node[b * N + k] = hf[0] / N * u0 * u0;
+        double s = 0.0;
+        for (int m = 1; m <= N - 2; ++m) {
+            const double um = vt[(size_t)rank[m] * N + k];
+            s += hf[m] / N * um * um;
+        }
+        hse_node[b * N + k] = s;
+    }
+    if (sv_out)
+        for (int m = tid; m < N; m += kThreads) sv_out[b * N + m] = lam[rank[m]];
+}
+
+size_t hma_modes_lds_bytes(int N) { return sizeof(double) * 2 * (size_t)N + sizeof(int) * 6 * (size_t)N; }
+
 size_t hma_lds_bytes(int N) {
     const int Np = N + (N & 1), P = Np / 2;
     return sizeof(double) * (2 * (size_t)Np * Np + 2 * P + Np + kThreads + Np) + sizeof(int) * (2 * Np + 4 * Np);
@@ -258,6 +371,23 @@ int wc_hma(int B, int N, double* fc, double* hin, double* hse, double* hin_node,
     hipLaunchKernelGGL(hma_kernel, dim3(B), dim3(kThreads), lds, static_cast<hipStream_t>(stream), N, fc, hin, hse,
                        hin_node, hse_node, clus_num, sv);
     return wc_hip_check("wc_hma");
+}
+
+int wc_hma_modes(int B, int N, const double* lam, const double* vt, double* hin, double* hse, double* hin_node,
+                 double* hse_node, int* clus_num, double* sv, void* stream) {
+    wc_clear_err();
+    if (B <= 0 || N < 3 || !lam || !vt || !hin || !hse || !hin_node || !hse_node)
+        return wc_set_err(WC_EINVAL, "wc_hma_modes: bad B/N or NULL argument");
+    const size_t lds = hma_modes_lds_bytes(N);
+    if (lds > 160 * 1024) return wc_set_err(WC_EUNSUPPORTED, "wc_hma_modes: N too large for the LDS label arrays");
+    if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute((const void*)hma_modes_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+        if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(hma_modes_kernel, dim3(B), dim3(kThreads), lds, static_cast<hipStream_t>(stream), N, lam, vt,
+                       hin, hse, hin_node, hse_node, clus_num, sv);
+    return wc_hip_check("wc_hma_modes");
 }
 
 }  // extern "C"

@@ -32,7 +32,8 @@
 #include "wc_common.h"
 #include "wc_device.h"
 
-// N > 96: wc_sde_large.hip (one GEMM-shaped launch per Euler step)
+// N > 96: wc_sde_large.hip (fp32: one persistent cooperative launch, the state in registers;
+// fallback and fp64: one GEMM-shaped launch per Euler step)
 size_t wc_large_workspace_size(int B, int N, int precision);
 int wc_large_integrate(const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
                        const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,

@@ -617,14 +617,18 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
 // connectome rows of its 128 nodes (read-only: LDS-DMA, as in step_kernel) and the whole E
 // image of its 80 simulations, which the 8 node-block workgroups of the simulation block
 // publish every step (every node's E feeds every node's coupling).  The hand-off follows
-// MI355X_MICROARCH.md's validated form (row 1 of its sc1 table): the E image is stored
-// write-through (buffer stores, sc1) and read with sc1 buffer loads only; every storing wave
-// drains vmcnt before a workgroup barrier, after which one lane adds 1 to the simulation
-// block's counter (agent-scope atomic); the consumer's one lane polls that counter with sc1
-// loads, then a workgroup barrier releases the other waves.  One workgroup per CU (the grid
-// never exceeds the CU count and the LDS footprint admits one per CU): every workgroup is
-// resident, so the per-block waits cannot deadlock; every wait is still bounded (a timeout
-// sets the error word and poisons the state with NaN instead of hanging the device).
+// MI355X_MICROARCH.md's fence-free form (its "Valid forms" consumer conditions (1)-(4) with
+// row 1 of the sc1 hand-off table; DESIGN.md 3.1b quotes them): the E image is stored
+// write-through (8-B sc1 buffer stores) and every load of it is a 16-B sc1 buffer load to
+// registers; every storing wave drains vmcnt before a workgroup barrier, after which ONE lane
+// adds 1 to the simulation block's counter (a relaxed agent-scope atomic add -- no release
+// fence: the sc1 stores have left the CU once vmcnt drained); the consumer's one lane polls that
+// counter with relaxed agent-scope (sc1) loads, then a workgroup barrier releases the other
+// waves (no acquire fence: every image load bypasses the L1).  Co-residency of the whole grid
+// (one workgroup per CU) is guaranteed by the cooperative launch, which fails instead of
+// running partly resident (the host then falls back to step_kernel).  Every wait is still
+// bounded: a timeout sets the error word, the state is poisoned with NaN, and the host reads
+// the word back and returns WC_EHIP.
 // Double-buffered E image: a block writes E(s+1) into the buffer read at step s-1, which
 // every block of its simulation block has finished reading (it passed that block's step-s
 // wait).  The arithmetic per cell -- K order of the MFMA chain, the epilogue expressions,
@@ -632,6 +636,7 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
 constexpr int kPN = 128, kPS = 80, kPT = kPS / 16;  // nodes, simulations, simulation tiles per workgroup
 constexpr int kPWaves = kPN / 16;                     // 8
 constexpr uint32_t kSpinLimit = 1u << 22;             // polls per wait before giving up (~seconds)
+constexpr int kPersistRetry = 1;                      // run_persistent: cooperative launch refused
 #ifndef WC_PPAIR
 #define WC_PPAIR 1
 #endif
@@ -774,9 +779,9 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         }
     }
     if (!my_uni) uni = 0;  // benign race: every writer stores 0
-    // publish this wave's E tiles into image `buf` and release them to the simulation block:
-    // write-through stores, a vmcnt drain in every storing wave, a workgroup barrier, one lane's
-    // agent-scope release and counter add (MI355X_MICROARCH.md "Valid forms", producer)
+    // publish this wave's E tiles into image `buf` and signal the simulation block:
+    // write-through (sc1) stores, a vmcnt drain in every storing wave, a workgroup barrier, one
+    // lane's relaxed agent-scope counter add (the fence-free form above: no release fence)
     auto publish = [&](int buf) {
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
@@ -793,8 +798,9 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    // consumer: one lane polls the counter (relaxed, sc1 loads), then ONE agent acquire, a vmcnt
-    // wait and a workgroup barrier before any wave loads the image (bounded: error word + exit)
+    // consumer: one lane polls the counter (relaxed agent-scope = sc1 loads), then a workgroup
+    // barrier before any wave loads the image, every such load sc1 (no acquire fence; bounded:
+    // error word + exit)
     auto wait_for = [&](unsigned target) -> bool {
         if (DIAG == 4) {
             __syncthreads();
@@ -991,8 +997,8 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             if (b < g.B && n < g.N) {
                 const size_t o = (size_t)b * g.N + n;
                 a.E[o] = poisoned ? __builtin_nan("") : (double)E[t][r];
-                a.I[o] = (double)I[t][r];
-                a.A[o] = Av[t][r].get();
+                a.I[o] = poisoned ? __builtin_nan("") : (double)I[t][r];
+                a.A[o] = poisoned ? __builtin_nan("") : Av[t][r].get();
             }
         }
     }
@@ -1052,20 +1058,38 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
     hipError_t me = hipMemsetAsync(a.ws + g.o_cnt, 0, g.o_err + al(4) - g.o_cnt, st);  // counters + error word
     if (me != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(me));
     const dim3 grid((unsigned)(g.SBp * g.NBp)), blk(kPWaves * 64);
+    const void* kern = (const void*)persist_kernel<0>;
 #ifdef WCSDE_DIAG
     const char* env = getenv("WCSDE_PERSISTENT");
     switch (env ? env[0] : '1') {
-        case '2': hipLaunchKernelGGL(persist_kernel<1>, grid, blk, 0, st, a); break;
-        case '3': hipLaunchKernelGGL(persist_kernel<2>, grid, blk, 0, st, a); break;
-        case '4': hipLaunchKernelGGL(persist_kernel<3>, grid, blk, 0, st, a); break;
-        case '5': hipLaunchKernelGGL(persist_kernel<4>, grid, blk, 0, st, a); break;
-        default: hipLaunchKernelGGL(persist_kernel<0>, grid, blk, 0, st, a);
+        case '2': kern = (const void*)persist_kernel<1>; break;
+        case '3': kern = (const void*)persist_kernel<2>; break;
+        case '4': kern = (const void*)persist_kernel<3>; break;
+        case '5': kern = (const void*)persist_kernel<4>; break;
+        default: break;
     }
-#else
-    hipLaunchKernelGGL(persist_kernel<0>, grid, blk, 0, st, a);
 #endif
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
+    // cooperative: the whole grid is co-resident (the inter-workgroup waits need it) or the launch
+    // fails -- e.g. another process holds CUs -- and the caller runs step_kernel instead
+    void* kargs[] = {&a};
+    hipError_t e = hipLaunchCooperativeKernel(kern, grid, blk, kargs, 0, st);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return kPersistRetry;
+    }
+    // the hand-off's error word: a wait that timed out poisoned the state (NaN); report it
+    // instead of returning plausible partial records (one stream sync per call, >= 2 steps)
+    static thread_local unsigned* herr = nullptr;
+    if (!herr && hipHostMalloc((void**)&herr, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) herr = nullptr;
+    if (!herr) return wc_set_err(WC_EHIP, "wc_integrate: pinned host word for the persistent error check");
+    *herr = 0;
+    if ((e = hipMemcpyAsync(herr, a.ws + g.o_err, sizeof(unsigned), hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return wc_set_err(WC_EHIP, hipGetErrorString(e));
+    if (*herr)
+        return wc_set_err(WC_EHIP, "wc_integrate: persistent N > 96 integrator: an inter-workgroup wait timed out "
+                                   "(state poisoned with NaN)");
+    return WC_OK;
 }
 
 }  // namespace
@@ -1085,9 +1109,11 @@ int wc_large_integrate(const wc_params* p, int precision, int B, int N, const do
     if (precision == WC_F64)
         return run_large<double>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld,
                                  recE, recI, recA, workspace, st);
-    if (nsteps > 1 && persistent_ok(B, N))
-        return run_persistent(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld, recE,
-                              recI, recA, workspace, st);
+    if (nsteps > 1 && persistent_ok(B, N)) {
+        const int rc = run_persistent(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld,
+                                      recE, recI, recA, workspace, st);
+        if (rc != kPersistRetry) return rc;  // else: the grid could not be made co-resident
+    }
     return run_large<float>(p, B, N, sc, G, sigmaE, keys, E, I, A, step0, nsteps, tau_ip, rec_every, rec_ld, recE,
                             recI, recA, workspace, st);
 }

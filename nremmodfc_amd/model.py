@@ -110,6 +110,12 @@ class Batch:
         self.params = params or driver_params()
         self.precision = precision
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is not None and \
+                self.device.index != torch.cuda.current_device():
+            # libwcsde launches on torch's current stream of the CURRENT device: a batch on
+            # another GPU would get kernels on the wrong device's stream (fail, do not guess)
+            raise ValueError(f"Batch on {self.device} but the current device is cuda:{torch.cuda.current_device()}: "
+                             f"call torch.cuda.set_device({self.device.index}) first")
         sc = torch.as_tensor(np.asarray(sc, dtype=np.float64)).to(self.device).contiguous()
         if sc.ndim != 2 or sc.shape[0] != sc.shape[1]:
             raise ValueError("sc must be N x N")

@@ -93,10 +93,35 @@ def _params():
                     rI=rI, mu=mu, sigmaI=sigmaI, D=D, dtSim=dtSim, dt=dt)
 
 
-def _wilsonCowan(*args, **kw):
-    """The reference's per-step RHS (wc:77-83) is fused into the integrator kernel
-    (wc_integrate); a single-step host evaluation is deliberately not offered."""
-    raise NotImplementedError("wilsonCowan is fused into run()/wc_integrate; call run()")
+_rhs_step = 0  # Philox step of the next wilsonCowan() call: each call draws fresh noise (wc:80)
+
+
+def _wilsonCowan(t, X, sigmaE, mu, tau_ip, G):
+    """wilsonCowan(t, X, sigmaE, mu, tau_ip, G) of wc:77-83 -> (3, N) float64 derivatives
+    (dE/dt, dI/dt, da_ie/dt), evaluated on the device (wc_rhs).  Like the reference it draws
+    new noise on every call: the normals of Philox step 0, 1, 2, ... of the `sid` stream
+    (the integrator's normals at those global steps).  `t` is unused, as in the reference."""
+    global _rhs_step
+    from . import _lib
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    cm = np.asarray(CM, dtype=np.float64)
+    n = cm.shape[0]
+    if X.shape != (3, n):
+        raise ValueError(f"X must be (3, N) = (3, {n}) rows (E, I, a_ie)")
+    p = _params()
+    p.mu = float(mu)
+    dev = torch.device(device)
+    tens = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
+    g = tens(np.broadcast_to(np.asarray(G, dtype=np.float64), (n,)))
+    s = tens(np.broadcast_to(np.asarray(sigmaE, dtype=np.float64), (n,)))
+    keys = torch.from_numpy(sim_keys([sid], [0]).view(np.int64).copy()).to(dev)
+    x = tens(X)
+    out = torch.empty_like(x)
+    rc = _lib.lib().wc_rhs(p.to_c(), 1, n, _lib.ptr(tens(cm)), _lib.ptr(g), _lib.ptr(s), _lib.ptr(keys),
+                           _rhs_step, float(tau_ip), _lib.ptr(x), _lib.ptr(out), _lib.stream_handle())
+    _lib.check(rc, "wc_rhs")
+    _rhs_step += 1
+    return out.cpu().numpy()
 
 
 wilsonCowan = _Recompilable(_wilsonCowan)

@@ -147,9 +147,35 @@ def hma(fc, want_clus_num=False):
     out = {k: torch.empty(s, dtype=torch.float64, device=dev)
            for k, s in (("hin", (B,)), ("hse", (B,)), ("hin_node", (B, N)), ("hse_node", (B, N)), ("sv", (B, N)))}
     cn = torch.empty((B, N - 1), dtype=torch.int32, device=dev) if want_clus_num else None
-    rc = L.wc_hma(B, N, _lib.ptr(fc), _lib.ptr(out["hin"]), _lib.ptr(out["hse"]), _lib.ptr(out["hin_node"]),
-                  _lib.ptr(out["hse_node"]), _lib.ptr(cn), _lib.ptr(out["sv"]), _lib.stream_handle())
-    _lib.check(rc, "wc_hma")
+    if N <= HMA_JACOBI_MAX_N:
+        rc = L.wc_hma(B, N, _lib.ptr(fc), _lib.ptr(out["hin"]), _lib.ptr(out["hse"]), _lib.ptr(out["hin_node"]),
+                      _lib.ptr(out["hse_node"]), _lib.ptr(cn), _lib.ptr(out["sv"]), _lib.stream_handle())
+        _lib.check(rc, "wc_hma")
+        return _with_cn(out, cn)
+    # N > 96: F and V no longer fit one workgroup's LDS.  The eigensystem of the symmetrised
+    # positive part comes from the batched device eigensolver (rocSOLVER through torch.linalg.eigh),
+    # everything after it -- ranks, module levels, Balance, nodal measures -- from wc_hma_modes.
+    fc.clamp_(min=0.0)  # HMA.py:55: the caller's FC is clipped in place
+    for b0 in range(0, B, HMA_EIGH_BATCH):
+        b1 = min(B, b0 + HMA_EIGH_BATCH)
+        f = fc[b0:b1]
+        lam, V = torch.linalg.eigh((f + f.transpose(1, 2)) / 2)
+        vt = V.transpose(1, 2).contiguous()  # row j = eigenvector j (coalesced rows per level)
+        sl = {k: v[b0:b1] for k, v in out.items()}
+        rc = L.wc_hma_modes(b1 - b0, N, _lib.ptr(lam.contiguous()), _lib.ptr(vt), _lib.ptr(sl["hin"]),
+                            _lib.ptr(sl["hse"]), _lib.ptr(sl["hin_node"]), _lib.ptr(sl["hse_node"]),
+                            _lib.ptr(cn[b0:b1] if cn is not None else None), _lib.ptr(sl["sv"]),
+                            _lib.stream_handle())
+        _lib.check(rc, "wc_hma_modes")
+        del lam, V, vt
+    return _with_cn(out, cn)
+
+
+HMA_JACOBI_MAX_N = 96   # wc_hma: F and V (2 N^2 fp64) in one workgroup's LDS
+HMA_EIGH_BATCH = 64     # N > 96: matrices per eigensolver call (bounds the V buffers)
+
+
+def _with_cn(out, cn):
     if cn is not None:
         out["clus_num"] = cn
     return out

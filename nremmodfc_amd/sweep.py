@@ -322,9 +322,12 @@ def main(argv=None):
     if launcher == "slurm":
         local %= max(1, torch.cuda.device_count())
     device = f"cuda:{local}"
+    # every launcher: the library launches on torch's current stream and queries the current
+    # HIP device (CU count, occupancy), so the current device must be this rank's GPU
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
     if launcher == "torch" and world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     os.makedirs(os.path.join(args.out, "temp"), exist_ok=True)
     sims, tag = _sim_list(args)

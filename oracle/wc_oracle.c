@@ -25,10 +25,14 @@
  *   noise = sqdtD * z  ==  np.random.normal(0, sqdtD, N)   (wc:80)
  *
  * Parity status: the arithmetic of S/wilsonCowan/run is restated line by line
- * (cited above); the reference module cannot be imported here (numba absent,
- * BOLDModel absent -- SURVEY.md 8c), so the integrator is pinned statistically
- * against the reference's shipped sweep outputs (tests/test_statistics_*.py),
- * not bit-for-bit.
+ * (cited above) and pinned to the reference's OWN run(): tests/golden/
+ * make_ref_replay.py executes /root/reference/netwWilsonCowanPlastic.py with its
+ * numba decorators as identities and np.random.normal replaying this Philox
+ * stream; tests/test_oracle_ref_replay.py checks this loop
+ * against that Y_t at <= 1e-13 (observed 3e-15: np.dot/np.exp rounding).  Over
+ * the full 1001 s schedule it is also pinned statistically to the reference's
+ * shipped sweep tables (tests/test_oracle_pin.py, tests/golden/oracle_pin_cell.json).
+ * BOLD (orc_bold) remains unpinned: BOLDModel is absent from the reference.
  */
 #include <math.h>
 #include <stdint.h>

@@ -39,7 +39,7 @@ def test_product_library_has_no_diagnostic_entry_points():
 def test_abi_version_and_workspace():
     from nremmodfc_amd import _lib
     L = _lib.lib()
-    assert L.wcsde_abi_version() == 4
+    assert L.wcsde_abi_version() == 5
     # N <= 96: sized for the 3-part 16-bit image (the fp16x2 image and its two scale floats fit inside)
     assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16
     assert L.wc_workspace_size(20000, 90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
@@ -91,6 +91,19 @@ def test_hma_validates_without_device_work():
     assert L.wc_hma(4, 90, None, vp, vp, vp, vp, None, None, None) == -1
     assert L.wc_hma(4, 97, vp, vp, vp, vp, vp, None, None, None) == -2
     assert b"96" in L.wc_last_error()
+    # N > 96 goes through wc_hma_modes (caller's eigensystem): it validates before launching too
+    assert L.wc_hma_modes(4, 1000, None, vp, vp, vp, vp, vp, None, None, None) == -1
+    assert L.wc_hma_modes(4, 2, vp, vp, vp, vp, vp, vp, None, None, None) == -1
+    assert L.wc_hma_modes(1, 20000, vp, vp, vp, vp, vp, vp, None, None, None) == -2
+
+
+def test_rhs_validates_without_device_work():
+    from nremmodfc_amd import _lib
+    L = _lib.lib()
+    p = _lib.WCParamsC()
+    vp = ctypes.c_void_p(16)
+    assert L.wc_rhs(ctypes.byref(p), 0, 90, vp, vp, vp, vp, 0, 1.0, vp, vp, None) == -1
+    assert L.wc_rhs(ctypes.byref(p), 1, 90, vp, vp, vp, vp, 1 << 48, 1.0, vp, vp, None) == -2
 
 
 def test_corrcoef_validates_without_device_work():

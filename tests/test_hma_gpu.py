@@ -59,6 +59,27 @@ def test_hma_matches_host_facade(cuda, N, B):
         np.testing.assert_allclose(r["sv"][b].cpu().numpy(), sv, rtol=1e-11, atol=1e-13)
 
 
+@pytest.mark.parametrize("N,B", [(97, 3), (150, 2), (301, 2)])
+def test_hma_large_n_matches_host_facade(cuda, N, B):
+    """N > 96 (HMA.py has no N cap): the device eigensolver + wc_hma_modes vs the host facade
+    (the reference's algorithm, numpy SVD)."""
+    rng = np.random.default_rng(N * 7 + B)
+    fcs = _fc_like(rng, B, N)
+    t = torch.from_numpy(fcs.copy()).to(cuda)
+    r = sigchain.hma(t, want_clus_num=True)
+    for b in range(B):
+        f = fcs[b].copy()
+        cn, cs, _ = HMA.Functional_HP(f)
+        hin, hse = HMA.Balance(f, cn, cs)
+        hin_n, hse_n = HMA.nodal_measures(f, cn, cs)
+        np.testing.assert_array_equal(r["clus_num"][b].cpu().numpy(), cn)
+        np.testing.assert_allclose(r["hin"][b].item(), hin, rtol=1e-11)
+        np.testing.assert_allclose(r["hse"][b].item(), hse, rtol=1e-10)
+        np.testing.assert_allclose(r["hin_node"][b].cpu().numpy(), hin_n, rtol=1e-9, atol=1e-14)
+        np.testing.assert_allclose(r["hse_node"][b].cpu().numpy(), hse_n, rtol=1e-8, atol=1e-14)
+        np.testing.assert_array_equal(t[b].cpu().numpy(), f)  # clipped in place, as HMA.py:55
+
+
 def test_hma_batch_is_order_independent(cuda):
     rng = np.random.default_rng(5)
     fcs = _fc_like(rng, 6, 90)

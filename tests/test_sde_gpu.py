@@ -278,4 +278,4 @@ def test_matches_reference_run_replay(cuda, sc90, prec, name):
     if prec == "f64":
         assert mx <= 1e-9, diff.max(axis=(0, 2))
     else:
-        assert mx <= 1e-3 and rms <= 3e-5, (mx, rms)
+        assert mx <= 5e-4 and rms <= 1.2e-5, (mx, rms)  # observed max 4.8e-5, rms 1.1e-6 (2200 steps)

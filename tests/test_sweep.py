@@ -253,6 +253,26 @@ def test_sweep_main_n1000_short(tmp_path, cuda):
 
 
 @pytest.mark.gpu
+def test_many_seeds_main_n1000_short(tmp_path, cuda):
+    """run_many_seeds.py at N = 1000 (HMA.py has no N cap): the driver integrates, then the
+    N > 96 HMA path (device eigensolver + wc_hma_modes) produces every pickle entry."""
+    import pickle
+    out = str(tmp_path)
+    sweep.main(["many", "--modality", "homo", "--seeds", "1", "--short", "--nodes", "1000", "--out", out,
+                "--tag", "m1k"])
+    with open(os.path.join(out, "m1k.pickle"), "rb") as f:  # our own file
+        d = pickle.load(f)
+    assert d["metainfo"] == {s: 1 for s in datasets.STATES}
+    v = d[(0, "N2")]
+    assert v["sFC"].shape == (1000, 1000) and (v["sFC"] >= 0).all()
+    assert v["Hse_node_sim"].shape == (1000,) and np.isfinite(v["Hin_sim"]) and np.isfinite(v["Hse_sim"])
+    from nremmodfc_amd import HMA
+    h = HMA.integration_segregation(d[(0, "W")]["sFC"].copy())
+    np.testing.assert_allclose(d[(0, "W")]["Hin_sim"], h["Hin_sim"], rtol=1e-10)
+    np.testing.assert_allclose(d[(0, "W")]["Hse_sim"], h["Hse_sim"], rtol=1e-9)
+
+
+@pytest.mark.gpu
 def test_many_seeds_full_size(tmp_path, cuda):
     """Config 2 at full size: run_many_seeds.py's 50 seeds x 4 states at the map optima over
     the full 1001 s schedule (run_many_seeds.py:105-146) -> the collapsed pickle, read the way
