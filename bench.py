@@ -68,14 +68,51 @@ def sweep_batch(rank, n_seeds=50, nG=20, nS=20):
 CPU_SHARE = 16  # host cores one GPU's job may use on the GPU box (its OMP_NUM_THREADS / MAX_JOBS)
 
 
-def cpu_baseline(sc, seconds=15.0, steps=2000):
-    """The oracle's C restatement of run() on the host cores (kind 'port')."""
-    import oracle
+def _cores():
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count()
-    ncores = max(1, min(avail, CPU_SHARE))
+    return avail, max(1, min(avail, CPU_SHARE))
+
+
+def cpu_baseline_numpy(steps=150_000):
+    """The reference's own hot loop as NumPy executes it (oracle/numpy_run.py: wc:72-137 operation
+    for operation, bit-identical to the reference's run() under the same normals), one
+    single-threaded process per core as the reference's SLURM array runs it,
+    truncated horizon (per-step cost is constant).  Workers are child processes started with
+    subprocess (numpy only, OPENBLAS/OMP/MKL_NUM_THREADS=1)."""
+    import subprocess
+    avail, ncores = _cores()
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    t0 = time.perf_counter()
+    procs = [subprocess.Popen([sys.executable, "-m", "oracle.numpy_run", str(steps), str(i)], cwd=ROOT, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True) for i in range(ncores)]
+    secs = []
+    for pr in procs:
+        out, _ = pr.communicate()
+        if pr.returncode != 0:
+            raise RuntimeError("cpu_baseline_numpy: a worker failed")
+        secs.append(float(out.strip().splitlines()[-1]))
+    wall = time.perf_counter() - t0
+    per_core = [90 * steps / s for s in secs]
+    value = 90 * steps * ncores / max(secs)  # every worker's node-steps over the slowest worker's loop time
+    return {"value": value, "unit": "node-timesteps/sec", "cores": ncores, "kind": "port",
+            "cores_available": avail, "cores_cap": CPU_SHARE,
+            "per_core": {"mean": float(np.mean(per_core)), "min": float(min(per_core))},
+            "extrapolated_all_available_cores": float(np.mean(per_core)) * avail,
+            "sample": f"{ncores} processes x 1 sim x {steps} Euler steps of the C3 cell (0.16, 7.68), N=90: the "
+                      f"reference's NumPy loop (oracle/numpy_run.py, bit-identical to netwWilsonCowanPlastic.py's "
+                      f"run() under replayed noise), numpy's normal draws, 1 BLAS thread each; {wall:.1f} s wall",
+            "note": "cores capped at one GPU's host share on the box (CPU_SHARE); extrapolated_all_available_cores "
+                    "= mean per-core rate x cores_available, not measured"}
+
+
+def cpu_baseline_compiled(sc, seconds=8.0, steps=2000):
+    """The oracle's compiled C restatement of run() (oracle/wc_oracle.c), OpenMP over simulations:
+    the per-step cost of a compiled loop, as numba gives the reference (kind 'port')."""
+    import oracle
+    avail, ncores = _cores()
     G, S, keys = sweep_batch(0)
     p = driver_params()
     B = 2 * ncores
@@ -91,8 +128,17 @@ def cpu_baseline(sc, seconds=15.0, steps=2000):
     ns = B * sc.shape[0] * steps * n
     return {"value": ns / total, "unit": "node-timesteps/sec", "cores": ncores, "kind": "port",
             "cores_available": avail, "cores_cap": CPU_SHARE,
+            "extrapolated_all_available_cores": ns / total / ncores * avail,
             "sample": f"{B} sims x {steps * n} Euler steps of the C3 grid (tau_ip=2, E recorded every "
                       f"20 steps), oracle/wc_oracle.c fp64, OpenMP over simulations, {total:.1f} s"}
+
+
+def cpu_baseline(sc, seconds=8.0, steps=2000):
+    """The reference-shaped NumPy leg (the reported baseline) with the compiled C port beside it;
+    `seconds` sizes both (about 2 x seconds of CPU work in total)."""
+    out = cpu_baseline_numpy(steps=max(2000, int(seconds * 20_000)))
+    out["compiled_port"] = cpu_baseline_compiled(sc, seconds, steps)
+    return out
 
 
 def main():
@@ -109,7 +155,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="weak: 20,000 (c3) / 2,500 (c5) sims per rank; strong: the one c3 sweep (20,000 sims) or "
                          "c5 sweep (20,000 sims over 8 GPUs = 2,500 x 8) split round-robin over the ranks")

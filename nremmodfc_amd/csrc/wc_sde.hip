@@ -164,13 +164,18 @@ struct PkConsts {
 #ifndef WC_INC2
 #define WC_INC2 1
 #endif
+// LEAN (V_LEAN): a_ie as a two-part running sum without per-step compensation -- lo collects
+// the increments (one add), the value used is hi + lo (one add), and the caller folds lo into
+// hi every 16 steps (renorm_a) -- two operations per cell pair fewer than Kahan-Babuska, the
+// same value to within an fp32 rounding of a_ie.  AII0 (V_AII0): a_ii == 0 (the reference's
+// value, wc:25), so the inhibitory sigmoid's in * cIi term, exactly cI0 + 0, is dropped.
 #pragma clang fp contract(off)
-template <bool ES = false>
+template <bool ES = false, bool LEAN = false, bool AII0 = false>
 __device__ __forceinline__ void cell_pair_f32(const PkConsts& k, f2v& e, f2v& in, f2v& ahi, f2v& alo, f2v cpl,
                                               f2v G, f2v sl, f2v z) {
     const f2v e0 = e, in0 = in;
     f2v x = __builtin_elementwise_fma(k.a_ee, e0, k.Pm);
-    x = __builtin_elementwise_fma(-ahi, in0, x);
+    x = __builtin_elementwise_fma(LEAN ? -(ahi + alo) : -ahi, in0, x);
     x = __builtin_elementwise_fma(G, cpl, x);
     x = __builtin_elementwise_fma(k.knoise, z, x);
     const f2v te = x * sl;
@@ -179,7 +184,8 @@ __device__ __forceinline__ void cell_pair_f32(const PkConsts& k, f2v& e, f2v& in
     constexpr float kS = ES ? 0x1p-10f : 1.0f;
     const f2v de = ES ? __builtin_elementwise_fma(ex, f2v{kS, kS}, f2v{kS, kS}) : one + ex;
     const f2v SE = {__builtin_amdgcn_rcpf(de.x), __builtin_amdgcn_rcpf(de.y)};
-    const f2v ti = __builtin_elementwise_fma(e0, k.cIe, __builtin_elementwise_fma(in0, k.cIi, k.cI0));
+    const f2v ti = AII0 ? __builtin_elementwise_fma(e0, k.cIe, k.cI0)
+                        : __builtin_elementwise_fma(e0, k.cIe, __builtin_elementwise_fma(in0, k.cIi, k.cI0));
     const f2v di = 1.0f + f2v{__builtin_amdgcn_exp2f(ti.x), __builtin_amdgcn_exp2f(ti.y)};
     const f2v SI = {__builtin_amdgcn_rcpf(di.x), __builtin_amdgcn_rcpf(di.y)};
     // (a_ie first: e0 and in0 are last read by their own updates, which can then write in place)
@@ -189,10 +195,14 @@ __device__ __forceinline__ void cell_pair_f32(const PkConsts& k, f2v& e, f2v& in
     const f2v tA = in0 * k.dtA;
     const f2v inc = __builtin_elementwise_fma(e0, tA, -k.rhoE * tA);
 #endif
-    const f2v t = inc + alo;  // Kahan-Babuska, as AccA<true>::add
-    const f2v s = ahi + t;
-    alo = t - (s - ahi);
-    ahi = s;
+    if constexpr (LEAN) {
+        alo = alo + inc;
+    } else {
+        const f2v t = inc + alo;  // Kahan-Babuska, as AccA<true>::add
+        const f2v s = ahi + t;
+        alo = t - (s - ahi);
+        ahi = s;
+    }
     // (ES: SE and e0 both carry 2^10, rE 2^-10: the same roundings times 2^10)
     e = __builtin_elementwise_fma(k.dtE, __builtin_elementwise_fma(__builtin_elementwise_fma(-k.rE, e0, one), SE, -e0), e0);
     in = __builtin_elementwise_fma(k.dtI, __builtin_elementwise_fma(__builtin_elementwise_fma(-k.rI, in0, one), SI, -in0), in0);
@@ -218,6 +228,8 @@ enum : int {
     V_MIX = 16384,    // NT = 6 over NW = 4 waves per group, two waves with 2 tiles and two with 1,
                       // the pattern rotated per group so the SIMDs of a 3-group workgroup carry
                       // 5/4/5/4 tiles instead of 6/4/4/4 (3 waves of 2 tiles)
+    V_LEAN = 32768,   // packed fp32 update: a_ie as hi + lo running sum, renormalised every 16 steps
+    V_AII0 = 65536,   // a_ii == 0 (host-checked): the inhibitory sigmoid without its in * cIi term
 };
 
 constexpr bool kFragRegs_(int var) { return (var & V_FRAG_REGS) != 0; }
@@ -250,6 +262,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     // the fp16x3 packed product path keeps E in units of 2^-10 (E[][] holds E 2^10): the
     // MFMA operand split needs no scaling multiply (cell_pair_f32<true>)
     constexpr bool kEs = kFast && kPk && kHf;
+    constexpr bool kLean = kFast && kPk && (VAR & V_LEAN) != 0;
+    constexpr bool kAii0 = kFast && kPk && (VAR & V_AII0) != 0;
     constexpr float kEsc = kEs ? 1024.0f : 1.0f, kEinv = kEs ? 0x1p-10f : 1.0f;
     // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
     constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
@@ -581,7 +595,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     f2v e = {E[u][r], E[u][r + 1]}, in = {I[u][r], I[u][r + 1]};
                     f2v ahi = {A[u][r].hi, A[u][r + 1].hi}, alo = {A[u][r].lo, A[u][r + 1].lo};
                     const f2v cpl = kMfma ? f2v{acc[u][r], acc[u][r + 1]} : e * kEinv;
-                    cell_pair_f32<kEs>(pk, e, in, ahi, alo, cpl, f2v{Gc[u][r], Gc[u][r + 1]}, f2v{Sl[u][r], Sl[u][r + 1]}, zp[h]);
+                    cell_pair_f32<kEs, kLean, kAii0>(pk, e, in, ahi, alo, cpl, f2v{Gc[u][r], Gc[u][r + 1]},
+                                                      f2v{Sl[u][r], Sl[u][r + 1]}, zp[h]);
                     E[u][r] = e.x;
                     E[u][r + 1] = e.y;
                     I[u][r] = in.x;
@@ -658,6 +673,18 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     I[u][r] = in + dtI * (-in + (1 - rI * in) * SI);
                     A[u][r].add(dtA * (in * (e - rhoE)));
                 }
+            }
+        }
+        if constexpr (kLean) {
+            if ((s & 15) == 15) {  // fold the running increments into hi (wave-uniform branch)
+#pragma unroll
+                for (int u = 0; u < OT; ++u)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float hs = A[u][r].hi + A[u][r].lo;
+                        A[u][r].lo = A[u][r].lo - (hs - A[u][r].hi);
+                        A[u][r].hi = hs;
+                    }
             }
         }
         publish(buf ^ 1);
@@ -780,11 +807,14 @@ int cu_count() {
 // Many groups: ONE workgroup per CU holding SG = ceil(groups / CUs) groups that
 // share the LDS connectome image (<= 155 / 128 registers): every simulation is
 // resident at once (a single round of workgroups, no tail) at 3-4 waves/SIMD.
+// X: extra variant bits of every product kernel (V_AII0 when a_ii == 0, the reference's value:
+// -2.2% per C3 launch, bit-identical, tools/diag_variants.py 38 vs 41)
+template <int X>
 int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
-    constexpr int V = V_F16X3 | V_KAHAN_A;
+    constexpr int V = V_F16X3 | V_KAHAN_A | X;
     const int groups = (ka.B + kSims - 1) / kSims;
     const int cus = cu_count();
-    if (groups <= 2 * cus) return launch_v<float, 6, 6, kVarF32>(ka, sc, ws, st);
+    if (groups <= 2 * cus) return launch_v<float, 6, 6, kVarF32 | X>(ka, sc, ws, st);
     // node-major E-only recording (the sweep pipeline's ring): pairs of records per 8-B store
     const bool rec2 = ka.rec_every > 0 && ka.rec_ld > 0 && ka.rec_ld % 2 == 0 && !ka.recI && !ka.recA &&
                       ((uintptr_t)ka.recE & 7) == 0;
@@ -802,13 +832,18 @@ int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) 
     }
 }
 
-int launch_f32(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+template <int X>
+int launch_f32_x(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     switch ((tiles_for(ka.N) + 1) & ~1) {
-        case 2: return launch_v<float, 2, 1, kVarF32>(ka, sc, ws, st);
-        case 4: return launch_v<float, 4, 2, kVarF32>(ka, sc, ws, st);
-        case 6: return launch_f32_nt6(ka, sc, ws, st);
+        case 2: return launch_v<float, 2, 1, kVarF32 | X>(ka, sc, ws, st);
+        case 4: return launch_v<float, 4, 2, kVarF32 | X>(ka, sc, ws, st);
+        case 6: return launch_f32_nt6<X>(ka, sc, ws, st);
         default: return wc_set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
     }
+}
+
+int launch_f32(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+    return ka.a_ii == 0.0 ? launch_f32_x<V_AII0>(ka, sc, ws, st) : launch_f32_x<0>(ka, sc, ws, st);
 }
 
 // fp64 parity path: one wave per node tile (NW = NT; E exchanged through LDS), so the
@@ -882,6 +917,10 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 38: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A, 1, 5>(ka, sc, ws, st);
         case 39: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_NO_RNG, 1, 5>(ka, sc, ws, st);
         case 40: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_NO_MFMA, 1, 5>(ka, sc, ws, st);
+        // round 3: the C3 product kernel (38) with the a_ii = 0 sigmoid (bit-identical), the lean a_ie sum, both
+        case 41: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_AII0, 1, 5>(ka, sc, ws, st);
+        case 42: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_LEAN, 1, 5>(ka, sc, ws, st);
+        case 43: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_LEAN | V_AII0, 1, 5>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }

@@ -74,8 +74,11 @@ def check_supported(N, schedule: Schedule = None, chunk_samples: int = 1000):
 def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedule: Schedule = None,
               params: WCParams = None, precision: str = F32, chunk_samples: int = 1000,
               bold_downsamp: int = 1000, max_launch_steps: int = 500_000, want_fc=False, want_bold=False,
-              device="cuda", progress=None) -> SweepResult:
-    """Run B simulations end to end and return the reference's per-simulation outputs."""
+              device="cuda", progress=None, init_state: Optional[Dict[str, np.ndarray]] = None) -> SweepResult:
+    """Run B simulations end to end and return the reference's per-simulation outputs.
+
+    init_state: optional {"E", "I", "A"} -> [B][N] initial state instead of run()'s
+    (0.1, 0.1, a_ie_0) (wc:90-99), e.g. to measure how a perturbation propagates."""
     sch = schedule or Schedule()
     p = params or driver_params()
     R = sch.rec_every
@@ -84,6 +87,8 @@ def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedul
     t_start = time.perf_counter()
     bt = Batch(sc, G, sigmaE, keys, p, precision, device)
     B, N = bt.B, bt.N
+    for name, x in (init_state or {}).items():
+        getattr(bt, name).copy_(torch.as_tensor(np.asarray(x, dtype=np.float64).reshape(B, N)))
     C = B * N
     # ---- transients (no recording) ----
     for n, tau in ((sch.n_trans1, sch.tau_ip[0]), (sch.n_trans2, sch.tau_ip[1])):

@@ -1,6 +1,7 @@
 """bench.py keeps the driver's JSON contract (task spec).
 
-CPU: the cpu_baseline leg (the oracle's C loop, kind "port") on a short sample.
+CPU: the cpu_baseline legs (the reference's NumPy loop, oracle/numpy_run.py, one process per
+core; the compiled C port beside it) on a short sample.
 GPU: one short bench run as a child process; its single JSON line carries every
 contract key, the roofline and issued-MFMA objects, and consistent arithmetic.
 """
@@ -20,8 +21,10 @@ def test_cpu_baseline_leg():
     from nremmodfc_amd import datasets
     cb = bench.cpu_baseline(datasets.load_sc(), seconds=0.3, steps=200)
     assert cb["kind"] == "port" and cb["unit"] == "node-timesteps/sec"
-    assert cb["value"] > 0 and 1 <= cb["cores"] <= 16 and "oracle/wc_oracle.c" in cb["sample"]
+    assert cb["value"] > 0 and 1 <= cb["cores"] <= 16 and "oracle/numpy_run.py" in cb["sample"]
     assert cb["cores"] == min(cb["cores_available"], cb["cores_cap"])
+    cp = cb["compiled_port"]
+    assert cp["value"] > 0 and "oracle/wc_oracle.c" in cp["sample"] and cp["cores"] == cb["cores"]
 
 
 @pytest.mark.gpu

@@ -279,3 +279,22 @@ def test_matches_reference_run_replay(cuda, sc90, prec, name):
         assert mx <= 1e-9, diff.max(axis=(0, 2))
     else:
         assert mx <= 5e-4 and rms <= 1.2e-5, (mx, rms)  # observed max 4.8e-5, rms 1.1e-6 (2200 steps)
+
+
+@pytest.mark.parametrize("B", [40, 20000])
+def test_f32_nonzero_a_ii(cuda, sc90, B):
+    """a_ii != 0 (the reference's a_ii = 0 selects the kernels without the in * cIi term, V_AII0):
+    the general fp32 kernels, small (register-resident) and grouped batches, vs the oracle."""
+    p = driver_params(a_ii=0.6)
+    keys = sim_keys(np.arange(B) % 50, np.arange(B) // 50)
+    G = np.full(B, 0.16)
+    gb = Batch(sc90, G, 7.68, keys, p, precision="f32")
+    ob = oracle.OracleBatch(sc90, G[-24:], 7.68, keys[-24:], p)
+    gb.integrate(100, 0.05)
+    ob.integrate(100, 0.05)
+    rec = torch.empty((10, B, 90), dtype=torch.float32, device="cuda")
+    gb.integrate(200, 2.0, 20, rec)
+    o = ob.integrate(200, 2.0, 20)
+    d = np.abs(rec[:, -24:].double().cpu().numpy().transpose(1, 0, 2) - o)
+    mx, rms = observed(d, f"a_ii-0.6-{B}")
+    assert mx <= 2e-6 and rms <= 3e-7, (mx, rms)

@@ -50,6 +50,7 @@ def main():
     G, S, keys = sweep_batch(0)
     # correctness (ablation variants 6/7 are expected to fail)
     ok = {}
+    first = {}  # the first variant's records: bit-identity of the others against it
     sG, sS, sk = G[:37], S[:37], keys[:37]
     ob = oracle.OracleBatch(sc, sG, sS, sk, p)
     ob.integrate(300, 0.05)
@@ -66,8 +67,9 @@ def main():
             diag(bt, v, 600, 2.0, 20, rec)
             got = rec.permute(1, 0, 2)
         torch.cuda.synchronize()
-        d = np.abs(got.double().cpu().numpy() - orec)
-        ok[v] = (float(d.max()), float(np.sqrt((d ** 2).mean())))
+        g = got.double().cpu().numpy()
+        d = np.abs(g - orec)
+        ok[v] = (float(d.max()), float(np.sqrt((d ** 2).mean())), bool(np.array_equal(g, first.setdefault("g", g))))
     # timing
     bt = Batch(sc, G, S, keys, p, precision="f32")
     rec = torch.empty((-(-steps // 20), bt.B, bt.N), dtype=torch.float32, device="cuda")
@@ -89,7 +91,8 @@ def main():
         ms = min(times[v])
         ns = bt.B * bt.N * steps / (ms * 1e-3)
         res.append({"variant": v, "ms": ms, "us_per_step": ms * 1e3 / steps, "node_steps_per_s": ns,
-                    "tflops_215": ns * 215 / 1e12, "max_err": ok[v][0], "rms_err": ok[v][1]})
+                    "tflops_215": ns * 215 / 1e12, "max_err": ok[v][0], "rms_err": ok[v][1],
+                    "bits_equal_first_variant": ok[v][2]})
         print(json.dumps(res[-1]), flush=True)
 
 
