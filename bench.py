@@ -38,6 +38,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 vector = FP32 matrix (MI355X_MICROARCH.
 PEAK_FP64_TFLOPS = 78.6
 PEAK_HBM_GBPS = 8000.0     # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAK_F16_TFLOPS = 2500.0   # dense fp16 MFMA (MI355X_MICROARCH.md); the fp16x3 coupling runs on it
+PEAK_IC_GATHER_GBPS = 8600.0  # rows gathered from the Infinity Cache into the CUs, chip-wide (MI355X_MICROARCH.md)
 
 
 def flops_per_node_step(N):
@@ -289,6 +290,17 @@ def main():
     traffic = pmc_d.get("hbm_bytes_per_launch")
     util = {k: pmc_d[k] for k in ("valu_insts_per_wave_step", "mfma_insts_per_wave_step", "mfma_busy_frac")
             if k in pmc_d}
+    if N > 96 and pmc_d:
+        # the persistent kernel's SQ counters come from their own PMC passes (tools/profile_c5_sq.sh)
+        sqf = os.path.join(ROOT, "profiles", "pmc_c5_sq.json")
+        try:
+            q = json.load(open(sqf)) if os.path.exists(sqf) else {}
+        except (ValueError, OSError):
+            q = {}
+        if q.get("kernel") == pmc_d.get("kernel"):
+            util.update({k: q[k] for k in ("mfma_busy_frac", "valu_issue_busy_frac", "salu_per_wave_step") if k in q})
+            util.update({f"{k.lower()}_per_wave_step": v for k, v in q.get("per_wave_step", {}).items()})
+            util["wave_cycle_split"] = q.get("wave_cycle_split")
     sq = pmc_d.get("sq", {})
     if sq.get("SQ_ACTIVE_INST_VALU") and sq.get("GRBM_GUI_ACTIVE"):
         # SQ_ACTIVE_INST_VALU counts quad-cycles per SIMD; GRBM_GUI_ACTIVE sums the 8 XCDs' clocks
@@ -334,9 +346,16 @@ def main():
                 "issued_f16_flops_per_node_step": ifl,
                 "algorithmic_tflops_fp32_equiv": per_launch_ns * fl / t_launch / 1e12,
                 "operand_stream": {"bytes_per_step": stream,
-                                   "GBps": stream * EULER / t_launch / 1e9},
-                "note": "fp16 MFMA roofline of the issued coupling work; the kernel is bound by the per-step "
-                        "operand stream from L2/Infinity Cache (operand_stream; ablation: 9.4 of 24.2 us per step). "
+                                   "GBps": stream * EULER / t_launch / 1e9,
+                                   "peak_GBps": PEAK_IC_GATHER_GBPS,
+                                   "frac": stream * EULER / t_launch / 1e9 / PEAK_IC_GATHER_GBPS,
+                                   "peak_note": "MI355X_MICROARCH.md 'Indexed rows: gather into LDS': rows of a "
+                                                "38 MB table from the Infinity Cache, 8.6 TB/s chip-wide (L2-resident "
+                                                "rows 16.8-18.8 TB/s)"},
+                "binding": "operand_stream",
+                "note": "fp16 MFMA roofline of the issued coupling work (frac); the kernel is bound by the per-step "
+                        "operand stream from L2/Infinity Cache, priced in operand_stream.frac against the Infinity-Cache "
+                        "row-gather rate (ablation without the K-loop loads: 14.8 of 24.2 us per step). "
                         "traffic = PMC FETCH+WRITE per launch; traffic_algorithmic = 24 B per node-step of "
                         "state streaming, which this kernel no longer moves"}
     roof["kernel_ms_per_launch"] = kern["sde"]

@@ -61,4 +61,6 @@ def test_bench_c5_line_priced_on_mfma(cuda):
     r = d["roofline"]
     assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1 and r["peak"] == 2500.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12 and r["operand_stream"]["GBps"] > 0
+    o = r["operand_stream"]
+    assert r["binding"] == "operand_stream" and abs(o["frac"] - o["GBps"] / o["peak_GBps"]) < 1e-12
     assert d["config"]["nodes"] == 1000 and d["config"]["sims_per_gpu"] == 2500
