@@ -96,20 +96,24 @@ __device__ __forceinline__ double fma3(double a, double b, double c) {
     asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
 }
-__device__ __forceinline__ double exp_rr(double x) {
-    const double k = __builtin_rint(x * 1.4426950408889634);
-    const double r = fma(-k, 1.9082149292705877e-10, fma(-k, 0.6931471803691238, x));  // ln2 hi + lo
-    double p = 2.505210838544172e-08;                                                  // 1/11!
-    p = fma3(p, r, 2.755731922398589e-07);
-    p = fma3(p, r, 2.7557319223985893e-06);
-    p = fma3(p, r, 2.48015873015873e-05);
-    p = fma3(p, r, 1.984126984126984e-04);
-    p = fma3(p, r, 1.388888888888889e-03);
-    p = fma3(p, r, 8.333333333333333e-03);
-    p = fma3(p, r, 4.1666666666666664e-02);
-    p = fma3(p, r, 1.6666666666666666e-01);
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
+// 2^y for the Balloon's (1 - E0)^(1/f) = 2^(log2(1 - E0) / f) (|y| < 1000): y = k + r, k = rint(y),
+// r = y - k exact (|r| <= 1/2), 2^r = e^(r ln2) by its degree-11 Taylor polynomial in r with the
+// ln2^n/n! folded into the coefficients (truncation < 7e-15 relative), 2^k by ldexp.  In base 2
+// the reduction is one exact subtraction (base e needed x log2e and a two-part ln2).
+__device__ __forceinline__ double exp2_rr(double y) {
+    const double k = __builtin_rint(y);
+    const double r = y - k;
+    double p = 4.4455382718708116e-10;  // ln2^11 / 11!
+    p = fma3(p, r, 7.054911620801123e-09);
+    p = fma3(p, r, 1.01780860092397e-07);
+    p = fma3(p, r, 1.321548679014431e-06);
+    p = fma3(p, r, 1.5252733804059841e-05);
+    p = fma3(p, r, 0.0001540353039338161);
+    p = fma3(p, r, 0.0013333558146428443);
+    p = fma3(p, r, 0.009618129107628477);
+    p = fma3(p, r, 0.05550410866482158);
+    p = fma3(p, r, 0.24022650695910072);
+    p = fma3(p, r, 0.6931471805599453);
     p = fma(p, r, 1.0);
     return __builtin_ldexp(p, (int)k);
 }
@@ -117,7 +121,8 @@ __device__ __forceinline__ double exp_rr(double x) {
 struct BoldArgs {
     wc_bold_cfg cfg;
     int64_t C, n, M;
-    double itaus, itauf, itauo, ialpha, iEo, vo, k1, k2, k3, log1mEo;
+    double itaus, itauf, itauo, ialpha, iEo, vo, k1, k2, k3, log2_1mEo;
+    double dq_a, dq_b;  // q += dq_a f (1 - fpow) - dq_b q v^(1/alpha - 1): dt itauo iEo, dt itauo
     double bc0, bc1, bc2, bc3;  // BOLD = vo (k1 (1-q) + k2 (1-q/v) + k3 (1-v)) = bc0 - bc1 q - bc2 q/v - bc3 v
     int alpha_3125;  // 1/alpha == 3.125: v^(1/alpha) = v^3 * v^(1/8) by square roots
 };
@@ -251,38 +256,38 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? 3 :
     // Balloon-Windkessel: BOLD[t] from the state after t steps, then one Euler step
     // driven by x (see oracle/wc_oracle.c orc_bold)
     auto balloon = [&](double x) -> double {
-        double iv, vpow, vpow_iv;
+        double iv, vpow_iv;
         if (STEADY || a.alpha_3125) {  // the host launches STEADY only when 1/alpha == 3.125
-            // z = v^(-1/8): fp32 seed (hardware sqrt/rsq), two division-free Newton steps
-            // z <- z (1 + (1 - v z^8)/8) (relative error ~1e-16); then 1/v = z^8 and
-            // v^(1/alpha) = v^3.125 = v^4 z^7
-            // (one Newton step from the ~3e-7 fp32 seed leaves ~4e-13 relative)
-            double z = (double)__builtin_amdgcn_rsqf(__builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf((float)v)));
-            {
-                const double z2 = z * z, z4 = z2 * z2;
-                z = fma(z * 0.125, fma(-v, z4 * z4, 1.0), z);
-            }
-            const double z2 = z * z, z4 = z2 * z2, z7 = z4 * z2 * z, v2 = v * v;
-            iv = z4 * z4;
-            vpow = v2 * v2 * z7;      // v^3.125
-            vpow_iv = v2 * v * z7;    // v^2.125 = vpow / v
+            // w = v^(-1/8) from an fp32 seed z (hardware sqrt/rsq, relative error ~3e-7) without
+            // a Newton update: with 1 - t = v z^8 (t = O(1e-6)),
+            //   1/v     = w^8 = z^8 / (1 - t)       = z^8 (1 + t + t^2 + O(t^3)),
+            //   v^(-7/8) = w^7 = z^7 (1 - t)^(-7/8) = z^7 (1 + 7t/8 + 105t^2/128 + O(t^3)),
+            // (relative error ~1e-17), v^2.125 = v^3 w^7 and v^3.125 = v v^2.125
+            const double z = (double)__builtin_amdgcn_rsqf(__builtin_amdgcn_sqrtf(__builtin_amdgcn_sqrtf((float)v)));
+            const double z2 = z * z, z4 = z2 * z2, z8 = z4 * z4;
+            const double t = fma(-v, z8, 1.0);
+            iv = fma(z8, fma(t, t, t), z8);
+            const double z7 = z4 * z2 * z;
+            const double w7 = fma(z7, fma(t, 0.8203125, 0.875) * t, z7);
+            vpow_iv = v * v * v * w7;  // v^2.125
         } else {
             iv = 1.0 / v;
-            vpow = exp(log(v) * a.ialpha);
-            vpow_iv = vpow * iv;
+            vpow_iv = exp(log(v) * a.ialpha) * iv;
         }
-        const double bold = fma(-a.bc3, v, fma(-a.bc2, q * iv, fma(-a.bc1, q, a.bc0)));
+        // bc0 - (bc1 q + bc2 q/v + bc3 v): every fma takes ONE uniform (SGPR) operand, so no
+        // constant is copied into a VGPR per sample (gfx950 VALU reads one scalar per instruction)
+        const double bold = a.bc0 - fma(a.bc1, q, fma(a.bc2, q * iv, a.bc3 * v));
         double rf = (double)__builtin_amdgcn_rcpf((float)f);  // 1/f: fp32 seed + one Newton step (~1e-14)
         rf = fma(rf, fma(-f, rf, 1.0), rf);
-        const double fpow = exp_rr(a.log1mEo * rf);  // (1 - E0)^(1/f)
+        const double fpow = exp2_rr(a.log2_1mEo * rf);  // (1 - E0)^(1/f)
         const double ds = x - a.itaus * s - a.itauf * (f - 1.0);
-        const double dv = (f - vpow) * a.itauo;
-        const double dq = (f * (1.0 - fpow) * a.iEo - q * vpow_iv) * a.itauo;
-        const double df = s;
+        // Euler steps with dt folded into the constants (dt itauo, dt itauo iEo):
+        //   v += dt (f - v^(1/alpha)) itauo;  q += dt (f (1 - fpow) iEo - q v^(1/alpha - 1)) itauo
+        const double vn = fma(a.dq_b, fma(-v, vpow_iv, f), v);
+        q = fma(a.dq_a, f * (1.0 - fpow), fma(-a.dq_b, q * vpow_iv, q));
+        f += dt * s;  // df = s (the state at the step's start)
         s += dt * ds;
-        f += dt * df;
-        v += dt * dv;
-        q += dt * dq;
+        v = vn;
         return bold;
     };
     // one sample of the stream (x = E at sample tt of this chunk), every case
@@ -331,17 +336,17 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? 3 :
     // (no divergent branch around it: the block counters and the table address stay
     // wave-uniform, in SGPRs; tail lanes of a COPY launch compute on a shadow column
     // and only their stores are masked)
-    auto steady = [&](double x, int64_t r, int64_t m) {  // r, m: (block position, block) of the sample
+    auto steady = [&](double x, int r, int m) {  // r, m: (block position, block) of the sample (32-bit, SGPRs)
         const double bold = balloon(x);
         const double y = BP ? iir_step_bp(zf, bold, b, fa) : iir_step(zf, bold, b, fa);
         const tab_ptr tab = tab_row(st, L, r);  // wave-uniform row: scalar loads
 #pragma unroll
         for (int j = 0; j < 5; ++j) acc[j] += tab[j] * y;
-        if (r == a.cfg.dec - 1) {
+        if (r == (int)a.cfg.dec - 1) {
             if (live) {
-                st[L.yzs + m * L.C + c] = acc[0];
+                st[L.yzs + (int64_t)m * L.C + c] = acc[0];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) st[L.u + (m * 4 + j) * L.C + c] = acc[1 + j];
+                for (int j = 0; j < 4; ++j) st[L.u + ((int64_t)m * 4 + j) * L.C + c] = acc[1 + j];
             }
 #pragma unroll
             for (int j = 0; j < 5; ++j) acc[j] = 0.0;
@@ -379,14 +384,17 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? 3 :
         if constexpr (COPY) {
             if (k0 == 0 && tb > 0) flush(tb - kCopyT, kCopyT);
         }
-        // STEADY: (position in block, block) of the batch's first sample, uniform scalars
-        const int64_t ib = t0 + tb - neq, dec = a.cfg.dec;
-        int64_t mb = STEADY ? ib / dec : 0, rb = STEADY ? ib - mb * dec : 0;
+        // STEADY: (position in block, block) of the batch's first sample, uniform 32-bit scalars
+        // (64-bit inequalities of scalars have no SALU compare and went to the VALU per sample)
+        const int64_t ib = t0 + tb - neq;
+        const int dec = (int)a.cfg.dec;
+        int mb = STEADY ? (int)(ib / dec) : 0, rb = STEADY ? (int)(ib - (int64_t)mb * dec) : 0;
+        const int rem = Tc - tb < 16 ? (int)(Tc - tb) : 16;  // samples of this batch inside the chunk
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             if constexpr (COPY) tile[lane * (kCopyT + 1) + k0 + j] = (float)x[j];
             if (STEADY) {
-                if (tb + j < Tc) steady((double)x[j], rb, mb);
+                if (j < rem) steady((double)x[j], rb, mb);
                 if (++rb == dec) {
                     rb = 0;
                     ++mb;
@@ -1002,7 +1010,9 @@ BoldArgs make_bold_args(const wc_bold_cfg* cfg, int64_t C) {
     a.k1 = 7.0 * Eo;
     a.k2 = 2.0;
     a.k3 = 2.0 * Eo - 0.2;
-    a.log1mEo = log(1.0 - Eo);
+    a.log2_1mEo = log2(1.0 - Eo);
+    a.dq_b = cfg->dt * a.itauo;
+    a.dq_a = cfg->dt * a.itauo * a.iEo;
     a.bc0 = a.vo * (a.k1 + a.k2 + a.k3);
     a.bc1 = a.vo * a.k1;
     a.bc2 = a.vo * a.k2;
