@@ -1,44 +1,67 @@
-"""north_star: "FC SSIM >= 0.999 vs reference at fixed seed" for the fp32 PRODUCT path over
-the real horizon -- the full 1001 s schedule, 298 BOLD samples, utils.py:48's data_range = 1.
+"""north_star: "FC SSIM >= 0.999 vs reference at fixed seed", measured at the reference's real
+horizon: the full 1001 s schedule, 298 BOLD samples, utils.py:48's data_range = 1.
 
-The fixed-seed reference is the fp64 pipeline: it follows the oracle (the restated
-reference loop, itself pinned to the shipped tables: test_oracle_pin.py) to <= 1e-9 on
-short horizons and to FC SSIM >= 0.999999 at 400k steps (test_pipeline_fc_ssim_vs_oracle).
-Over 1001 s the SDE is chaotic, so the fp32 and fp64 realisations of one seed decorrelate
-(a 1e-7 difference grows ~1e4-fold per second of model time): pathwise 0.999 is NOT
-reachable by any fp32 path.  Measured on MI355X (32 seeds at cell (0, 0),
-profiles/r02_fc_ssim_f32.json): same-seed SSIM(fp32 FC, fp64 FC) 0.861 (0.830-0.901),
-between-seed floor SSIM(fp64 seed s, fp64 seed s+1) 0.771; seed-averaged FCs fp32 vs fp64
-0.994 against a split-half fp64 floor of 0.979.  This test re-measures those numbers on
-16 seeds and checks what does hold: same-seed SSIM above the between-seed floor (the fp32
-path follows the same noise realisation) and the seed-averaged FC matching fp64 at the
-level of the fp64 split-half sampling floor.
+The reference at fixed seed is the reference's OWN run() (netwWilsonCowanPlastic.py:86-137 executed
+with np.random.normal replaying the build's Philox stream; tools/fc_horizon_ref.py ->
+tests/golden/ref_replay_full.npz, 32 keys of the W-optimum cell).  The same fixture holds the fp64
+C oracle fed the SAME normals: the two differ only in the rounding of np.dot / np.exp against a
+sequential C loop, and their FCs agree to SSIM 0.865 (0.82-0.91), not 0.999.  Their trajectories are
+fully decorrelated long before the recorded phase (max |dE| ~0.55 in its first second); a 1e-15
+perturbation of the initial state does the same (profiles/r03_fc_horizon.json).  So pathwise
+SSIM >= 0.999 at this horizon is reachable only by reproducing the reference's float operations bit
+for bit -- not by fp64, not by any fp32 path.  What holds, and is asserted here on 16 keys:
+  * the device pipeline, fp64 AND the fp32 product, is as close to the reference at the same seed
+    as the reference's own fp64 restatement is (same-noise floor ~0.866, far above the 0.771
+    between-seed floor);
+  * the seed-averaged FC matches the reference's at its own split-half sampling floor;
+  * every metric column's mean over seeds matches the reference's.
 """
+import os
+
 import numpy as np
 import pytest
 
 import oracle.sigchain as osg
 from nremmodfc_amd import datasets, sweep
-from nremmodfc_amd.model import Schedule, sim_keys
+from nremmodfc_amd.model import Schedule
 from nremmodfc_amd.pipeline import run_sweep
 
 pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_replay_full.npz")
+K = 16
 
 
-def test_f32_fc_ssim_full_schedule(cuda, sc90):
-    B = 16
-    sims = [s for s in sweep.homogeneous(B, 0) if (round(s.dG, 4), round(s.dsigma, 4)) == (0.0, 0.0)]
-    G = np.stack([s.G for s in sims])
-    S = np.stack([s.sigma for s in sims])
-    keys = sim_keys([s.seed for s in sims], [s.stream for s in sims])
+def _full(flat, n=90):
+    fc = np.eye(n)
+    iu = np.triu_indices(n, 1)
+    fc[iu] = flat
+    fc[iu[1], iu[0]] = flat
+    return fc
+
+
+def test_fc_same_seed_full_horizon_vs_reference_run(cuda, sc90):
+    fx = np.load(GOLD)
+    keys = fx["keys"][:K].astype(np.uint64)
+    ref = np.stack([_full(f) for f in fx["fc_ref"][:K]])
+    orc = np.stack([_full(f) for f in fx["fc_orc"][:K]])
     emp = {s: datasets.load_empfc(s) for s in datasets.STATES}
-    fc = {p: run_sweep(sc90, G, S, keys, emp, Schedule(), precision=p, want_fc=True).fc for p in ("f32", "f64")}
-    assert fc["f32"].shape == (B, 90, 90)
-    same = np.array([osg.ssim(fc["f32"][b], fc["f64"][b], 1.0) for b in range(B)])
-    floor = np.array([osg.ssim(fc["f64"][b], fc["f64"][(b + 1) % B], 1.0) for b in range(B)])
-    mean_fc = osg.ssim(fc["f32"].mean(0), fc["f64"].mean(0), 1.0)
-    half = osg.ssim(fc["f64"][:B // 2].mean(0), fc["f64"][B // 2:].mean(0), 1.0)
-    print(f"FC SSIM fp32 vs fp64, same seed: mean {same.mean():.4f} (min {same.min():.4f}); between seeds "
-          f"{floor.mean():.4f}; seed-mean FCs {mean_fc:.4f} (fp64 split-half floor {half:.4f})")
-    assert same.mean() > floor.mean() + 0.03
-    assert mean_fc >= half - 0.005
+    G, S = np.full(K, sweep.BASE_G), np.full(K, sweep.BASE_SIGMA)
+    ss = lambda A, B: np.array([osg.ssim(a, b, 1.0) for a, b in zip(A, B)])  # noqa: E731
+    floor_same = ss(orc, ref)                       # the reference's own fp64 restatement
+    floor_between = ss(ref, np.roll(ref, 1, axis=0))
+    half = osg.ssim(ref[:K // 2].mean(0), ref[K // 2:].mean(0), 1.0)
+    for prec in ("f64", "f32"):
+        r = run_sweep(sc90, G, S, keys, emp, Schedule(), precision=prec, want_fc=True)
+        same = ss(r.fc, ref)
+        mean_fc = osg.ssim(r.fc.mean(0), ref.mean(0), 1.0)
+        print(f"TOL fc-horizon-{prec}: same-seed SSIM vs reference {same.mean():.4f} (oracle's {floor_same.mean():.4f}, "
+              f"between seeds {floor_between.mean():.4f}); seed-mean FC {mean_fc:.4f} (split-half floor {half:.4f})")
+        assert same.mean() >= floor_same.mean() - 0.03          # observed: f64 0.867, f32 0.867 vs 0.865 (32 keys)
+        assert same.mean() >= floor_between.mean() + 0.05
+        assert mean_fc >= half - 0.005
+        cols = r.columns()
+        m = np.stack([cols[c] for c in sweep.METRIC_COLS], axis=1)
+        mref = fx["m_ref"][:K]
+        se = np.sqrt(2.0 / K) * mref.std(0, ddof=1)
+        z = np.abs(m.mean(0) - mref.mean(0)) / np.where(se > 0, se, 1)
+        assert z.max() < 4.0, dict(zip(sweep.METRIC_COLS, z.round(2)))

@@ -206,13 +206,12 @@ def test_pipeline_short_schedule_vs_oracle(cuda, sc90):
 
 
 def test_pipeline_fc_ssim_vs_oracle(cuda, sc90):
-    """North star: FC SSIM >= 0.999 vs the reference at fixed seed.  At fixed seed
-    this is the fp64 path (the oracle restates the reference loop with the same
-    Philox stream); it holds to ~1e-9.  The fp32 product path cannot be compared
-    pathwise over a sweep horizon: the SDE is chaotic (a 1e-7 difference grows
-    ~1e4-fold per second of model time, tests/test_sde_gpu.py), so fp32 and fp64
-    realisations of the same seed decorrelate -- it is validated statistically
-    against the shipped tables instead."""
+    """Pathwise FC parity of the fp64 pipeline with the oracle while the two trajectories are still
+    coherent: 2,200 transient + 400,000 recorded steps (18 BOLD samples), utils.py:48's
+    data_range = 1.  Beyond tens of seconds of model time two fp64 implementations that round
+    differently decorrelate (the oracle against the reference's own run() under the same noise
+    included); the full 1001 s horizon is tested against the reference's run() itself in
+    tests/test_fc_ssim_gpu.py."""
     from nremmodfc_amd.model import Schedule, driver_params, sim_keys
     from nremmodfc_amd.pipeline import run_sweep
     sch = Schedule(n_trans1=200, n_trans2=2000, n_sim=400_000)  # 18 BOLD samples
@@ -227,7 +226,7 @@ def test_pipeline_fc_ssim_vs_oracle(cuda, sc90):
     rec = ob.integrate(sch.n_sim, 2.0, 20)
     for b in range(len(keys)):
         _, _, wfc = osg.sim_metrics(rec[b], emp)
-        assert osg.ssim(res.fc[b], wfc, data_range=2.0) >= 0.999999
+        assert osg.ssim(res.fc[b], wfc, data_range=1.0) >= 0.999999
 
 
 @pytest.mark.parametrize("M,B,N", [(6000, 10, 90), (777, 3, 90), (65, 1, 7), (3, 2, 2), (6000, 300, 96)])
