@@ -29,6 +29,8 @@
 #include <stdio.h>
 #include <string.h>
 #include <algorithm>
+#include <mutex>
+#include <type_traits>
 #include "wc_common.h"
 #include "wc_device.h"
 
@@ -70,6 +72,13 @@ struct KArgs {
     int64_t rec_ld;  // 0: records [n_rec][B][N]; >0: node-major, (k, c) at c*rec_ld + k
     int nsteps;
     int B, N;
+    const float4* zbuf;  // V_ZMEM: this launch's raw normals, [step][tile][Bp][lane group] (zblock_kernel)
+    int zBp;             // simulations per step in zbuf (B rounded up to 16)
+    // V_ZMEM: workgroups blockIdx >= zgen_b0 run on the CUs the integrator leaves idle and draw the
+    // NEXT launch's normals (zgen_K steps from global step zgen_step0) into zbuf_next
+    float4* zbuf_next;
+    int zgen_b0, zgen_K;
+    int64_t zgen_step0;
 };
 
 // ---------------- A-operand (connectome) images ----------------
@@ -230,6 +239,7 @@ enum : int {
                       // 5/4/5/4 tiles instead of 6/4/4/4 (3 waves of 2 tiles)
     V_LEAN = 32768,   // packed fp32 update: a_ie as hi + lo running sum, renormalised every 16 steps
     V_AII0 = 65536,   // a_ii == 0 (host-checked): the inhibitory sigmoid without its in * cIi term
+    V_ZMEM = 131072,  // the raw normals come precomputed from zbuf (zblock_kernel on otherwise idle CUs)
 };
 
 constexpr bool kFragRegs_(int var) { return (var & V_FRAG_REGS) != 0; }
@@ -264,12 +274,27 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr bool kEs = kFast && kPk && kHf;
     constexpr bool kLean = kFast && kPk && (VAR & V_LEAN) != 0;
     constexpr bool kAii0 = kFast && kPk && (VAR & V_AII0) != 0;
+    constexpr bool kZMem = kFast && kPk && kRng && (VAR & V_ZMEM) != 0;
     constexpr float kEsc = kEs ? 1024.0f : 1.0f, kEinv = kEs ? 0x1p-10f : 1.0f;
     // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
     constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
     constexpr int kFragUnits = kBf ? NT * NC * PS : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if constexpr ((VAR & V_ZMEM) != 0) {
+        if ((int)blockIdx.x >= a.zgen_b0) {  // generator workgroup: the next block's normals, grid-stride
+            const uint32_t total = (uint32_t)a.zgen_K * NT * (uint32_t)a.zBp * 4u;
+            const uint32_t stride = (gridDim.x - a.zgen_b0) * blockDim.x;
+            for (uint32_t i = (blockIdx.x - a.zgen_b0) * blockDim.x + threadIdx.x; i < total; i += stride) {
+                const uint32_t gq = i & 3u, bq = (i >> 2) % (uint32_t)a.zBp, row = (i >> 2) / (uint32_t)a.zBp;
+                const uint32_t tq = row % NT, sq = row / NT;
+                f2v zp[2];
+                quad_normals_pk((uint64_t)(a.zgen_step0 + sq), 4u * tq + gq, a.keys[bq < (uint32_t)a.B ? bq : a.B - 1], zp);
+                a.zbuf_next[i] = make_float4(zp[0].x, zp[0].y, zp[1].x, zp[1].y);
+            }
+            return;
+        }
+    }
     // LDS: [A-operand image, unless kFragRegs] [E exchange, 2 buffers, if NW > 1]
     const size_t frag_bytes = kFragRegs ? 0 : (size_t)kFragUnits * 64 * (kBf ? 16 : sizeof(real4));
     const int grp = SG == 1 ? 0 : (threadIdx.x >> 6) / NW;
@@ -431,7 +456,20 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr int RB = (VAR & V_REC4) ? 4 : (VAR & V_REC2) ? 2 : 1;
     Real rbuf[RB > 1 ? OT : 1][4][RB > 1 ? RB - 1 : 1];
 
-    for (int s = 0; s < a.nsteps; ++s) {
+    // V_ZMEM: normals of the next kZD steps in flight
+    constexpr int kZD = kZMem ? 4 : 1;
+    float4 zq[kZD][kZMem ? OT : 1];
+    if constexpr (kZMem) {
+#pragma unroll
+        for (int d = 0; d < kZD; ++d)
+#pragma unroll
+            for (int u = 0; u < OT; ++u)
+                zq[d][u] = a.zbuf[(((size_t)min(d, a.nsteps - 1) * NT + TL(u)) * a.zBp + (size_t)b) * 4 + g];
+    }
+    // one Euler step; ZS = the V_ZMEM prefetch slot of step s (s % kZD: a compile-time index, so the
+    // in-flight normals are never moved between registers -- a move would wait for every older load)
+    auto step_body = [&](const int s, auto zslot) {
+        constexpr int ZS = decltype(zslot)::value;
         const int buf = s & 1;
         // ---- record the state before the update (wc:124-125) ----
         if (rec_every > 0) {
@@ -496,6 +534,17 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         int fl = lane;
         if constexpr (!kFragRegs || NW > 1) asm volatile("" : "+v"(fl));  // opaque: LDS reads stay in the loop
         const uint64_t gstep = (uint64_t)(a.step0 + s);
+        // V_ZMEM: this step's normals were loaded kZD steps ago (a step is shorter than a memory
+        // round trip); issue the load of step s + kZD now (clamped to the block's last step)
+        float4 zm[kZMem ? OT : 1];
+        if constexpr (kZMem) {
+            const int sl = min(s + kZD, a.nsteps - 1);
+#pragma unroll
+            for (int u = 0; u < OT; ++u) {
+                zm[u] = zq[ZS][u];
+                zq[ZS][u] = a.zbuf[(((size_t)sl * NT + TL(u)) * a.zBp + (size_t)b) * 4 + g];
+            }
+        }
         // V_ZFIRST: the normals do not depend on the coupling, so they can fill the MFMA chain's gaps
         float zz[kZFirst ? OT : 1][4];
         if constexpr (kZFirst) {
@@ -583,7 +632,10 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             Real z[4] = {0, 0, 0, 0};
             if constexpr (kFast && kPk) {
                 f2v zp[2] = {f2v{0, 0}, f2v{0, 0}};
-                if constexpr (kZFirst) {
+                if constexpr (kZMem) {
+                    zp[0] = f2v{zm[u].x, zm[u].y};
+                    zp[1] = f2v{zm[u].z, zm[u].w};
+                } else if constexpr (kZFirst) {
                     zp[0] = f2v{zz[u][0], zz[u][1]};
                     zp[1] = f2v{zz[u][2], zz[u][3]};
                 } else if constexpr (kRng) {
@@ -688,6 +740,21 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             }
         }
         publish(buf ^ 1);
+    };
+    if constexpr (kZMem) {
+        int s = 0;
+        for (; s + kZD <= a.nsteps; s += kZD) {
+            step_body(s, std::integral_constant<int, 0>{});
+            step_body(s + 1, std::integral_constant<int, 1 % kZD>{});
+            step_body(s + 2, std::integral_constant<int, 2 % kZD>{});
+            step_body(s + 3, std::integral_constant<int, 3 % kZD>{});
+        }
+        static_assert(kZD == 4, "the unrolled loop above assumes four slots");
+        if (s < a.nsteps) step_body(s++, std::integral_constant<int, 0>{});
+        if (s < a.nsteps) step_body(s++, std::integral_constant<int, 1 % kZD>{});
+        if (s < a.nsteps) step_body(s++, std::integral_constant<int, 2 % kZD>{});
+    } else {
+        for (int s = 0; s < a.nsteps; ++s) step_body(s, std::integral_constant<int, 0>{});
     }
 
     // ---- records still buffered (rec_row % RB of them): the newest are the last rbuf slots ----
@@ -737,10 +804,26 @@ __global__ void noise_kernel(const uint64_t* __restrict__ keys, int B, int N, in
         if (4 * q + r < N) out[(size_t)b * N + 4 * q + r] = z[r];
 }
 
+// The raw normals (quad_normals_pk, the integrator's own arithmetic: the same bits) of K steps for
+// V_ZMEM, laid out for the integrator's loads: z[step][tile t][simulation b][lane group g] is the
+// float4 of quad 4t + g of simulation b -- a wave's load for one tile is 1 KB contiguous.
+__global__ void __launch_bounds__(256) zblock_kernel(const uint64_t* __restrict__ keys, int B, int Bp, int NT,
+                                                     int64_t step0, float4* __restrict__ z) {
+    // grid: x over (simulation, lane group) pairs of a step, y = s * NT + t (32-bit index math only)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Bp * 4) return;
+    const int g = i & 3, b = i >> 2;
+    const int t = (int)(blockIdx.y % (unsigned)NT), s = (int)(blockIdx.y / (unsigned)NT);
+    f2v zp[2];
+    quad_normals_pk((uint64_t)(step0 + s), (uint32_t)(4 * t + g), keys[b < B ? b : B - 1], zp);
+    z[((size_t)blockIdx.y * Bp + b) * 4 + g] = make_float4(zp[0].x, zp[0].y, zp[1].x, zp[1].y);
+}
+
 int tiles_for(int N) { return (N + 15) / 16; }
 
 template <typename Real, int NT, int NW, int VAR, int MINW = 1, int SG = 1>
-int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st, bool prep = true, int extra_blocks = 0,
+             size_t lds_floor = 0) {
     constexpr bool hf = (VAR & V_F16X3) != 0;
     constexpr bool bf = (VAR & (V_BF16X6 | V_BF16X3)) != 0;
     constexpr bool frag_regs = (VAR & V_FRAG_REGS) != 0;
@@ -748,9 +831,11 @@ int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     if constexpr (hf) {
         const int total = NT * (NT / 2) * 64;
         float* scl = static_cast<float*>(ws) + hf_scale_offset(NT);
-        hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(1024), 0, st, sc, ka.N, scl);
-        hipLaunchKernelGGL((build_frag_f16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
-                           static_cast<const float*>(scl), static_cast<f16x8*>(ws));
+        if (prep) {  // (prep = false: a later launch of the same call reuses the image)
+            hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(1024), 0, st, sc, ka.N, scl);
+            hipLaunchKernelGGL((build_frag_f16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
+                               static_cast<const float*>(scl), static_cast<f16x8*>(ws));
+        }
         lds = (frag_regs ? 0 : (size_t)NT * (NT / 2) * 2 * 64 * 16) +
               (NW > 1 ? (size_t)SG * 2 * (NT / 2) * 2 * 64 * 16 : 0);
     } else if constexpr (bf) {
@@ -766,7 +851,8 @@ int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
         lds = (frag_regs ? 0 : (size_t)NT * NT * 64 * 4 * sizeof(Real)) +
               (NW > 1 ? (size_t)SG * 2 * NT * 64 * 4 * sizeof(Real) : 0);
     }
-    const int blocks = (ka.B + kSims * SG - 1) / (kSims * SG);
+    const int blocks = (ka.B + kSims * SG - 1) / (kSims * SG) + extra_blocks;
+    lds = std::max(lds, lds_floor);  // (a floor above half the CU's LDS: one workgroup per CU)
     auto kern = wc_sde_kernel<Real, NT, NW, VAR, MINW, SG>;
     if (lds > 65536) {
         hipError_t ea = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -791,6 +877,34 @@ size_t frag_bytes(int N, int precision) {
     return (size_t)nt * (nt / 2) * 3 * 64 * 16;
 }
 
+// the two normals blocks of the small-batch path follow the fp32 connectome image (256-B aligned)
+size_t zmem_offset(int N) { return (frag_bytes(N, WC_F32) + 255) / 256 * 256; }
+
+// ---- small batches: normals precomputed on the CUs the integrator leaves idle (V_ZMEM) ----
+// A strong-scaled shard (e.g. 2,500 simulations = 157 groups of 16 on 256 CUs) keeps only part of
+// the chip busy, and each busy CU's step is latency-bound; Philox + Box-Muller are about a third
+// of a tile's step.  Each launch covers kZK steps with one workgroup per CU: the integrating
+// workgroups read this block's normals from a buffer, the others draw the next block's
+// (double-buffered, ordered by the launches on one stream; launch_zmem).
+constexpr int kZK = 1000;                // steps per launch (a multiple of the drivers' rec_every 20)
+constexpr int kZMinIdle = 32;            // CUs the generator needs at least
+constexpr int kZMaxGroups = 160;         // measured regime: up to 2,560 simulations (the 8-way C3 shard)
+
+int cu_count();
+
+size_t zmem_block_bytes(int B) {
+    const int Bp = (B + kSims - 1) / kSims * kSims;
+    return (size_t)kZK * kMaxTiles * Bp * 4 * sizeof(float4);
+}
+
+// B and N for which the small-batch path precomputes its normals (fp32, 81 <= N <= 96)
+bool zmem_eligible_shape(int B, int N) {
+    const char* env = getenv("WCSDE_ZMEM");
+    if (env && env[0] == '0') return false;
+    const int groups = (B + kSims - 1) / kSims;
+    return tiles_for(N) == kMaxTiles && groups <= std::min(kZMaxGroups, cu_count() - kZMinIdle);
+}
+
 int cu_count() {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -807,6 +921,42 @@ int cu_count() {
 // Many groups: ONE workgroup per CU holding SG = ceil(groups / CUs) groups that
 // share the LDS connectome image (<= 155 / 128 registers): every simulation is
 // resident at once (a single round of workgroups, no tail) at 3-4 waves/SIMD.
+template <int X>
+int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int groups, int cus) {
+    // one launch per block of kZK steps on the caller's stream, ONE workgroup per CU (an LDS floor
+    // above half the CU's LDS): the first `groups` workgroups integrate this block from the buffered
+    // normals, the other cus - groups draw the next block's normals into the other buffer.  The
+    // first block's normals come from one zblock_kernel launch over the whole chip.
+    const int Bp = groups * kSims;
+    const size_t R = (size_t)ka.rec_every;
+    float4* zb[2] = {const_cast<float4*>(ka.zbuf), const_cast<float4*>(ka.zbuf) + zmem_block_bytes(ka.B) / sizeof(float4)};
+    const int K0 = std::min(kZK, ka.nsteps);
+    hipLaunchKernelGGL(zblock_kernel, dim3((unsigned)((Bp * 4 + 255) / 256), (unsigned)(K0 * kMaxTiles)), dim3(256), 0, st,
+                       ka.keys, ka.B, Bp, kMaxTiles, ka.step0, zb[0]);
+    const int nb = (ka.nsteps + kZK - 1) / kZK;
+    for (int k = 0; k < nb; ++k) {
+        KArgs kb = ka;
+        kb.step0 = ka.step0 + (int64_t)k * kZK;
+        kb.nsteps = std::min(kZK, ka.nsteps - k * kZK);
+        kb.zbuf = zb[k & 1];
+        kb.zBp = Bp;
+        kb.zbuf_next = zb[(k + 1) & 1];
+        kb.zgen_b0 = groups;
+        kb.zgen_step0 = kb.step0 + kZK;
+        kb.zgen_K = k + 1 < nb ? std::min(kZK, ka.nsteps - (k + 1) * kZK) : 0;
+        if (R) {  // this block's first record row (kZK is a multiple of rec_every)
+            const size_t row = (size_t)k * kZK / R;
+            const size_t off = ka.rec_ld ? row : row * (size_t)ka.B * ka.N;
+            kb.recE = static_cast<float*>(ka.recE) + off;
+            if (ka.recI) kb.recI = static_cast<float*>(ka.recI) + off;
+            if (ka.recA) kb.recA = static_cast<float*>(ka.recA) + off;
+        }
+        const int rc = launch_v<float, 6, 6, kVarF32 | X | V_ZMEM>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);
+        if (rc != WC_OK) return rc;
+    }
+    return wc_hip_check("wc_integrate (normals-block path)");
+}
+
 // X: extra variant bits of every product kernel (V_AII0 when a_ii == 0, the reference's value:
 // -2.2% per C3 launch, bit-identical, tools/diag_variants.py 38 vs 41)
 template <int X>
@@ -814,7 +964,12 @@ int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) 
     constexpr int V = V_F16X3 | V_KAHAN_A | X;
     const int groups = (ka.B + kSims - 1) / kSims;
     const int cus = cu_count();
-    if (groups <= 2 * cus) return launch_v<float, 6, 6, kVarF32 | X>(ka, sc, ws, st);
+    if (groups <= 2 * cus) {
+        if (groups <= std::min(kZMaxGroups, cus - kZMinIdle) && ka.nsteps >= 2 * kZK && ka.zbuf &&
+            (ka.rec_every == 0 || kZK % ka.rec_every == 0))
+            return launch_zmem<X>(ka, sc, ws, st, groups, cus);
+        return launch_v<float, 6, 6, kVarF32 | X>(ka, sc, ws, st);
+    }
     // node-major E-only recording (the sweep pipeline's ring): pairs of records per 8-B store
     const bool rec2 = ka.rec_every > 0 && ka.rec_ld > 0 && ka.rec_ld % 2 == 0 && !ka.recI && !ka.recA &&
                       ((uintptr_t)ka.recE & 7) == 0;
@@ -921,6 +1076,12 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 41: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_AII0, 1, 5>(ka, sc, ws, st);
         case 42: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_LEAN, 1, 5>(ka, sc, ws, st);
         case 43: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_LEAN | V_AII0, 1, 5>(ka, sc, ws, st);
+        // the small-batch product kernel (6 waves, one tile each) and its ablations: coupling MFMAs off,
+        // noise off, both off (where the latency-bound step of a strong-scaling shard goes)
+        case 44: return launch_v<float, 6, 6, kVarF32 | V_AII0>(ka, sc, ws, st);
+        case 45: return launch_v<float, 6, 6, kVarF32 | V_AII0 | V_NO_MFMA>(ka, sc, ws, st);
+        case 46: return launch_v<float, 6, 6, kVarF32 | V_AII0 | V_NO_RNG>(ka, sc, ws, st);
+        case 47: return launch_v<float, 6, 6, kVarF32 | V_AII0 | V_NO_MFMA | V_NO_RNG>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
@@ -949,6 +1110,10 @@ int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const 
     ka.G = G; ka.sigmaE = sigmaE; ka.keys = keys; ka.E = E; ka.I = I; ka.A = A;
     ka.frag = workspace; ka.recE = recE; ka.recI = recI; ka.recA = recA;
     ka.step0 = step0; ka.rec_every = rec_every; ka.rec_ld = rec_ld; ka.nsteps = (int)nsteps; ka.B = B; ka.N = N;
+    ka.zbuf = nullptr;
+    ka.zBp = 0;
+    if (precision == WC_F32 && zmem_eligible_shape(B, N) && ws_bytes >= zmem_offset(N) + 2 * zmem_block_bytes(B))
+        ka.zbuf = reinterpret_cast<const float4*>(static_cast<char*>(workspace) + zmem_offset(N));
     return WC_OK;
 }
 
@@ -966,7 +1131,8 @@ size_t wc_workspace_size(int B, int N, int precision) {
     // the diagnostic f32-MFMA variants need the native image; size for the larger
     const int nt = tiles_for(N);
     const size_t native = (size_t)nt * nt * 64 * 4 * (precision == WC_F64 ? 8 : 4);
-    const size_t need = frag_bytes(N, precision);
+    size_t need = frag_bytes(N, precision);
+    if (precision == WC_F32 && zmem_eligible_shape(B, N)) need = zmem_offset(N) + 2 * zmem_block_bytes(B);
     return need > native ? need : native;
 }
 

@@ -70,7 +70,9 @@ def main():
         g = got.double().cpu().numpy()
         d = np.abs(g - orec)
         ok[v] = (float(d.max()), float(np.sqrt((d ** 2).mean())), bool(np.array_equal(g, first.setdefault("g", g))))
-    # timing
+    # timing (DIAG_B: batch size, default the C3 batch)
+    nb = int(os.environ.get("DIAG_B", len(keys)))
+    G, S, keys = G[:nb], S[:nb], keys[:nb]
     bt = Batch(sc, G, S, keys, p, precision="f32")
     rec = torch.empty((-(-steps // 20), bt.B, bt.N), dtype=torch.float32, device="cuda")
     recn = torch.empty((bt.B * bt.N, (-(-steps // 20) + 3) // 4 * 4), dtype=torch.float32, device="cuda")
