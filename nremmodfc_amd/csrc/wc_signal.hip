@@ -179,8 +179,12 @@ __device__ __forceinline__ void emit(const BoldArgs& a, const BoldLayout& L, dou
 // COPY: time-major fp32 input, also written out node-major (copy[c*copy_ld + tt])
 // through a 256-column x 32-sample LDS tile flushed as 128-B rows.
 constexpr int kCopyT = 32;
+#ifndef WC_BOLD_COPY_WPS
+#define WC_BOLD_COPY_WPS 4  // workgroups (of 4 waves) per CU for the steady copy instantiation: 128 VGPRs,
+                            // 8 spilled, 6% faster than 3 (tools/ab_multi.sh, profiles/r03_ab_bold.log)
+#endif
 template <typename ET, bool COPY, bool STEADY, bool BP = false>
-__global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? 3 : 4) : 1) bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, int64_t e_ld,
+__global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? WC_BOLD_COPY_WPS : 4) : 1) bold_chunk_kernel(const BoldArgs a, const ET* __restrict__ E, int64_t e_ld,
                                                          int64_t t0, int64_t Tc, double* __restrict__ st,
                                                          float* __restrict__ copy, int64_t copy_ld) {
     const int64_t c0 = (int64_t)blockIdx.x * blockDim.x;
