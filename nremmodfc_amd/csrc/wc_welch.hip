@@ -567,11 +567,26 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         wstage1(z, x, hann, ln);
         // the Hann loads have retired: the next column's loads are the only VMEM in flight
         const int nn = n + kWv < ncol ? n + kWv : n;
+#if defined(WC_WELCH_DIAG_NOLOAD)  // (ablation builds only: tools/dbg/welch_variants.sh)
+        (void)nn;
+#else
         WELCH_FETCH(nn, 0, kPfEarly, ln);
+#endif
+#if defined(WC_WELCH_DIAG_NOFFT)
+        {
+            const f2 v = ldsr(z + ln);
+            acc[0][0] += v.x;
+            acc[0][1] += v.y;
+        }
+        WELCH_FETCH(nn, kPfEarly, 7, ln);
+#else
         wstage<5, 5, kTb2>(z, Ts, ln);
         wstage<5, 25, kTb3>(z, Ts, ln);
+#if !defined(WC_WELCH_DIAG_NOLOAD)
         WELCH_FETCH(nn, kPfEarly, 7, ln);  // (the rest of the next column: fewer live registers through the stages)
+#endif
         wstage_last_unpack(z, Ts, Tu, acc, ln);
+#endif
     }
 #undef WELCH_FETCH
     // ---- combine each simulation's four waves (fp64) into its accumulator row (single writer) ----
@@ -595,6 +610,240 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
 #pragma unroll
         for (int v = 0; v < kWv; ++v) sacc += (double)red[(sw * kWv + v) * kBins + k];
         a.acc[(int64_t)bs * kBins + k] += 0.25 * sacc;
+    }
+}
+
+// ---------------- fp32 product kernel, two waves per column ----------------
+// The one-wave kernel above holds 16 KB of LDS per column in flight and 232 VGPRs, so a CU
+// runs 8 columns on 8 waves, two per SIMD, and each column's stages are one wave's serial
+// chain of LDS round trips (latency-bound, PMC: VALU issue 55% busy).  Here a PAIR of waves
+// shares a column: stages 1-3 split the 7 butterfly rows 4 + 3 between them, and the radix-16
+// last stage gives each lane ONE butterfly b: the lower half-wave holds b = m, the upper
+// half-wave its unpack partner b = 125 - m in the same lane pair (m = 0 pairs with a virtual
+// butterfly 125: butterfly 0 read with twiddles T^(250 r) = W16^r, i.e. its outputs rotated by
+// one slot, Z_{125 (s + 1)}).  Two half-exchanges per slot pair (v_permlane32_swap) hand each
+// lane its partner's slots 8..15, so every lane unpacks 8 bin pairs with no select.  Workgroup
+// = one simulation, 4 column pairs (8 waves, 80 KB of LDS), two workgroups per CU: 16 waves at
+// <= 128 VGPRs.  Six workgroup barriers per column (the pair's in-place stages need
+// read -> barrier -> write -> barrier); the other workgroup on the CU runs between them.
+#ifndef WC_WELCH_PAIR
+#define WC_WELCH_PAIR 0
+#endif
+constexpr int kPairCols = 4;                       // column pairs per workgroup
+constexpr int kPairThreads = kPairCols * 2 * 64;   // 512
+constexpr int kP4 = 126;                           // last-stage table width: butterflies 0..125
+constexpr int kPTs2 = 0, kPTs3 = kPTs2 + 4 * 5, kPTs4 = kPTs3 + 4 * 25;
+constexpr int kPTw = kPTs4 + 15 * kP4;             // 2010 stage twiddles
+constexpr size_t kPairLds = (size_t)kPairCols * kFFT * 8 + (size_t)kPTw * 8 + 2 * kPairCols * 4;  // 80,112 B
+
+// one radix-5 stage over rows q0 .. q0 + NQ - 1 of the 7 (P = 1: the windowed stage 1 from
+// registers; else in place from LDS with the table at TB): reads, barrier, products, writes
+template <int P, int NQ, int Q0>
+__device__ __forceinline__ void pstage_rw(f2* z, const f2* Ts, int TB, int lane) {
+    using R = Rows<5, P>;
+    f2 u[NQ][5];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int i = R::idx(lane, Q0 + q);
+#pragma unroll
+        for (int r = 0; r < 5; ++r) u[q][r] = ldsr(z + i + r * R::S);
+    }
+    __syncthreads();  // both waves' reads of the column precede either's in-place writes
+    f2 tw[2][4];
+#pragma unroll
+    for (int r = 1; r < 5; ++r) tw[0][r - 1] = ldsr(Ts + TB + R::idx(lane, Q0) % P + (r - 1) * P);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if (q + 1 < NQ) {
+#pragma unroll
+            for (int r = 1; r < 5; ++r) tw[(q + 1) & 1][r - 1] = ldsr(Ts + TB + R::idx(lane, Q0 + q + 1) % P + (r - 1) * P);
+        }
+#pragma unroll
+        for (int r = 1; r < 5; ++r) u[q][r] = cmulv(u[q][r], tw[q & 1][r - 1]);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int i = R::idx(lane, Q0 + q), k = i % P;
+        f2 U[5];
+        butterfly<5>(u[q], U);
+        const int j = (i - k) * 5 + k;
+        if (R::own(lane, Q0 + q)) {
+#pragma unroll
+            for (int s = 0; s < 5; ++s) z[j + s * P] = U[s];
+        }
+    }
+    __syncthreads();
+}
+
+// half-exchange between the wave's lane halves: afterwards a holds the partner lane's b and
+// b the partner's a (lanes l and l ^ 32), two v_permlane32_swap per dword
+__device__ __forceinline__ float2 swap_halves(float a, float b) {
+    const auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    const auto r2 = __builtin_amdgcn_permlane32_swap(r1[1], r1[0], false, false);
+    return make_float2(__uint_as_float(r2[1]), __uint_as_float(r2[0]));
+}
+__device__ __forceinline__ void swap_pair(f2& a, f2& b) {
+    const float2 x = swap_halves(a.x, b.x), y = swap_halves(a.y, b.y);
+    a = (f2){x.x, y.x};
+    b = (f2){x.y, y.y};
+}
+
+template <int H>
+__device__ __forceinline__ void pair_columns(const WelchArgs& a, f2* z, const f2* Ts, float* red, float* redf, int c,
+                                             int lane) {
+    constexpr int NQ = H == 0 ? 4 : 3, Q0 = H == 0 ? 0 : 4;  // stage 1-3 rows of this wave
+    const int b = blockIdx.x;
+    const int ncol = a.N;
+    const float* twg = reinterpret_cast<const float*>(a.tw + 2 * kSeg);
+    const f2* tw32 = reinterpret_cast<const f2*>(twg);
+    const f2* hann = tw32 + kSeg;
+    const float* E = static_cast<const float*>(a.E);
+    // last-stage butterfly of this lane: pair p = 32 H + lane % 32 (m = min(p, 62)), lower
+    // half b = m, upper half its partner 125 - m; valid pairs p <= 62
+    const int p = 32 * H + (lane & 31);
+    const int m = min(p, 62);
+    const int bl = lane < 32 ? m : 125 - m;
+    const int brd = bl == 125 ? 0 : bl;  // the virtual butterfly 125 reads butterfly 0
+    const f2 tb = tw32[bl];              // T^b: the unpack twiddles T^(b + 125 s) = T^b W32^s
+    float acc[8][2];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc[s][0] = acc[s][1] = 0.f;
+    const unsigned L = (unsigned)(a.slot * a.nslots);
+    const unsigned baseB = (unsigned)(a.seg0 % L) * 4u, LB = L * 4u;
+    const int64_t bc = (int64_t)b * ncol;
+    f2 x[NQ][5];
+#define PAIR_FETCH(n, QA, QB, LN)                                                              \
+    {                                                                                          \
+        const float* col_ = E + (bc + (n)) * a.ld;                                             \
+        _Pragma("unroll") for (int q = QA; q < QB; ++q) {                                      \
+            const int i_ = Rows<5, 1>::idx(LN, Q0 + q);                                       \
+            _Pragma("unroll") for (int r = 0; r < 5; ++r) {                                    \
+                unsigned o_ = baseB + 8u * (unsigned)(i_ + 400 * r);                           \
+                o_ = min(o_, o_ - LB);                                                         \
+                x[q][r] = *reinterpret_cast<const f2*>(reinterpret_cast<const char*>(col_) + o_); \
+            }                                                                                  \
+        }                                                                                      \
+    }
+    PAIR_FETCH(min(c, ncol - 1), 0, NQ, lane);
+    // every pair runs the same number of columns (barriers): the last round's missing columns
+    // repeat column ncol - 1 and are not accumulated
+    for (int n0 = 0; n0 < ncol; n0 += kPairCols) {
+        const int n = n0 + c;
+        const bool live = n < ncol;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        ln &= 63;
+        // ---- column mean (constant detrend): the pair's two partial sums ----
+        float part = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q)
+#pragma unroll
+            for (int r = 0; r < 5; ++r) part += Rows<5, 1>::own(ln, Q0 + q) ? x[q][r].x + x[q][r].y : 0.f;
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        if (ln == 0) red[2 * c + H] = part;
+        __syncthreads();  // (B1: also every wave's last-stage reads of the previous column are done)
+        const float mean = (red[2 * c] + red[2 * c + 1]) / (float)kSeg;
+        // ---- stage 1 (radix 5, no twiddles): detrend, periodic Hann window, butterflies ----
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = Rows<5, 1>::idx(ln, Q0 + q);
+            f2 U[5];
+#pragma unroll
+            for (int r = 0; r < 5; ++r) {
+                const f2 hw = *reinterpret_cast<const f2*>(reinterpret_cast<const char*>(hann) + (unsigned)(i + r * 400) * 8u);
+                x[q][r] = (x[q][r] - mean) * hw;
+            }
+            butterfly<5>(x[q], U);
+            if (Rows<5, 1>::own(ln, Q0 + q)) {
+#pragma unroll
+                for (int s = 0; s < 5; ++s) z[5 * i + s] = U[s];
+            }
+        }
+        const int nn = min(n + kPairCols, ncol - 1);
+        PAIR_FETCH(nn, 0, NQ - 1, ln);
+        __syncthreads();  // B2
+        pstage_rw<5, NQ, Q0>(z, Ts, kPTs2, ln);   // B3, B4
+        pstage_rw<25, NQ, Q0>(z, Ts, kPTs3, ln);  // B5, B6
+        PAIR_FETCH(nn, NQ - 1, NQ, ln);
+        // ---- last stage (radix 16, P = 125): one butterfly per lane, then the unpack ----
+        f2 u[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) u[r] = ldsr(z + brd + 125 * r);
+        f2 tw[15];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) tw[r - 1] = ldsr(Ts + kPTs4 + (r - 1) * kP4 + bl);
+#pragma unroll
+        for (int r = 1; r < 16; ++r) u[r] = cmulv(u[r], tw[r - 1]);
+        dft16(u);
+        // partner's slots 8..15: afterwards slot 8 + t holds the partner's 15 - t and v.v.
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            swap_pair(u[8 + t], u[15 - t]);
+        }
+        if (live) {
+            f2 tu = tb;
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                // W32^s = exp(-2 pi i s / 32)
+                constexpr float w32c[8] = {1.f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
+                                           0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
+                                           0.19509032201612826785f};
+                constexpr float w32s[8] = {0.f, 0.19509032201612826785f, 0.38268343236508977173f, 0.55557023301960222474f,
+                                           0.70710678118654752440f, 0.83146961230254523708f, 0.92387953251128675613f,
+                                           0.98078528040323044913f};
+                if (s > 0) tu = cmulv(tb, (f2){w32c[s], -w32s[s]});
+                const f2 Zk = u[s], Zc = u[8 + s];
+                f2 sv, dv;
+                asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
+                asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
+                const f2 pv = cmulv(dv, tu);
+                const f2 xa = add_mi(sv, pv), xb = sub_mi(sv, pv);
+                acc[s][0] = sq_acc(xa.x, sq_acc(xa.y, acc[s][0]));
+                acc[s][1] = sq_acc(xb.x, sq_acc(xb.y, acc[s][1]));
+            }
+        }
+    }
+#undef PAIR_FETCH
+    __syncthreads();  // the column buffers become the reduction area
+    // bins once each: pairs p <= 62; of the pair (0, 125) the virtual butterfly gives bin 1000 only
+    const bool okp = p <= 62;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const int k0 = bl + 125 * s, k1 = kFFT - bl - 125 * s;
+        const bool virt = bl == 125;
+        if (okp && (!virt || s == 7)) redf[c * kBins + k0] = acc[s][0];
+        if (okp && !virt) redf[c * kBins + k1] = acc[s][1];
+    }
+}
+
+__global__ void __launch_bounds__(kPairThreads, 4) welch_pair_kernel(const WelchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int c = wg >> 1, h = wg & 1;
+    f2* z = reinterpret_cast<f2*>(smem) + c * kFFT;
+    f2* Ts = reinterpret_cast<f2*>(smem) + kPairCols * kFFT;
+    float* red = reinterpret_cast<float*>(Ts + kPTw);
+    float* redf = reinterpret_cast<float*>(smem);  // [kPairCols][kBins] after the column loop
+    {  // stage tables from the fp32 turn: entry (k, r) of the stage (P, RAD) = T^(r k 4000 / (P RAD))
+        const f2* tw32 = reinterpret_cast<const f2*>(a.tw + 2 * kSeg);
+        for (int i = threadIdx.x; i < kPTw; i += kPairThreads) {
+            int P, RAD, base, W;
+            if (i < kPTs3) { base = kPTs2; P = 5; RAD = 5; W = 5; }
+            else if (i < kPTs4) { base = kPTs3; P = 25; RAD = 5; W = 25; }
+            else { base = kPTs4; P = 125; RAD = 16; W = kP4; }
+            const int k = (i - base) % W, r = (i - base) / W + 1;
+            Ts[i] = tw32[(r * k * (kSeg / (P * RAD))) % kSeg];
+        }
+    }
+    __syncthreads();
+    if (h == 0) pair_columns<0>(a, z, Ts, red, redf, c, lane);
+    else pair_columns<1>(a, z, Ts, red, redf, c, lane);
+    __syncthreads();
+    for (int k = threadIdx.x; k < kBins; k += kPairThreads) {
+        double sacc = 0.0;
+#pragma unroll
+        for (int v = 0; v < kPairCols; ++v) sacc += (double)redf[v * kBins + k];
+        a.acc[(int64_t)blockIdx.x * kBins + k] += 0.25 * sacc;
     }
 }
 
@@ -667,11 +916,18 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
         hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
     } else {
         if (ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 && ld < INT32_MAX / 2 - 8192) {
+#if WC_WELCH_PAIR
+            hipError_t ea = hipFuncSetAttribute((const void*)welch_pair_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairLds);
+            if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
+            hipLaunchKernelGGL(welch_pair_kernel, dim3(B), dim3(kPairThreads), kPairLds, st, a);
+#else
             hipError_t ea = hipFuncSetAttribute((const void*)welch_wave_kernel,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWelchLds);
             if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
             hipLaunchKernelGGL(welch_wave_kernel, dim3((B + kSimsWg - 1) / kSimsWg), dim3(kWv * kSimsWg * 64),
                                kWelchLds, st, a);
+#endif
         } else {  // unaligned rings (e.g. odd lengths): the LDS-Stockham kernel, scalar loads
             const size_t lds = (size_t)2 * kG<float> * kFFT * sizeof(cx<float>) + 4 * kG<float> * sizeof(float);
             hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<float>,
