@@ -291,7 +291,7 @@ def main():
     util = {k: pmc_d[k] for k in ("valu_insts_per_wave_step", "mfma_insts_per_wave_step", "mfma_busy_frac")
             if k in pmc_d}
     if N > 96 and pmc_d:
-        # the persistent kernel's SQ counters come from their own PMC passes (tools/profile_c5_sq.sh)
+        # the persistent kernel's SQ counters come from their own PMC passes (tools/profile_c5_pass.sh sqa / sqb, tools/profile_c5_summary.py)
         sqf = os.path.join(ROOT, "profiles", "pmc_c5_sq.json")
         try:
             q = json.load(open(sqf)) if os.path.exists(sqf) else {}

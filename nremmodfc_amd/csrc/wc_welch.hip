@@ -627,8 +627,9 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
 // <= 128 VGPRs.  Six workgroup barriers per column (the pair's in-place stages need
 // read -> barrier -> write -> barrier); the other workgroup on the CU runs between them.
 #ifndef WC_WELCH_PAIR
-#define WC_WELCH_PAIR 0
+#define WC_WELCH_PAIR 0  // 1: build the two-waves-per-column kernel and launch it (ablation)
 #endif
+#if WC_WELCH_PAIR
 constexpr int kPairCols = 4;                       // column pairs per workgroup
 constexpr int kPairThreads = kPairCols * 2 * 64;   // 512
 constexpr int kP4 = 126;                           // last-stage table width: butterflies 0..125
@@ -846,6 +847,8 @@ __global__ void __launch_bounds__(kPairThreads, 4) welch_pair_kernel(const Welch
         a.acc[(int64_t)blockIdx.x * kBins + k] += 0.25 * sacc;
     }
 }
+
+#endif  // WC_WELCH_PAIR
 
 // mean PSD (density scaling, one-sided) and the first argmax -> peak frequency
 __global__ void welch_peak_kernel(int B, int N, int nseg, double fs, const double* __restrict__ acc,

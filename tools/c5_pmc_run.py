@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Short C5 integrator run for rocprofv3 --pmc passes (tools/profile_c5.sh): the bench's C5 shard
+"""Short C5 integrator run for rocprofv3 --pmc passes (tools/profile_c5_pass.sh): the bench's C5 shard
 (2,500 simulations of the (G, sigma) grid on the 1000-node synthetic connectome), STEPS Euler steps
 recording every 20th into a node-major ring like bench.py --config c5 --sde-only."""
 import os

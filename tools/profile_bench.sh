@@ -80,7 +80,7 @@ json.dump(sig, open("gpurun_out/prof/pmc_signal.json", "w"), indent=1)
 json.dump(d, open("gpurun_out/prof/pmc_sde.json", "w"), indent=1)  # gpurun merges gpurun_out/ back only
 print(json.dumps(d))
 PY
-cp $OUT/bench_kernel_stats.csv profiles/r02_bench_kernel_stats.csv 2>/dev/null || true
+cp $OUT/bench_kernel_stats.csv gpurun_out/prof/r03_bench_kernel_stats.csv 2>/dev/null || true
 # on the GPU box only gpurun_out/ travels back: copy gpurun_out/prof/pmc_sde.json and
 # gpurun_out/prof/bench_kernel_stats.csv into profiles/ afterwards
 tail -1 $OUT/trace.log

@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Summaries of the four C5 PMC passes (tools/profile_c5_pass.sh fetch|write|sqa|sqb, one gpurun call
+each, merged back under gpurun_out/prof_c5/), run on the CPU from the repo root:
+  profiles/pmc_sde_c5.json  HBM bytes per persist_kernel step, scaled to bench.py's 20,000-step launch
+  profiles/pmc_c5_sq.json   instruction mix, MFMA / VALU busy and the wave-cycle split per wave-step"""
+def hbm():
+    import json, os, sys
+    sys.path.insert(0, "tools")
+    from pmc_summary import summary
+    (kf, vf), = summary("gpurun_out/prof_c5/fetch", "persist_kernel").items()
+    (kw, vw), = summary("gpurun_out/prof_c5/write", "persist_kernel").items()
+    B, N, STEPS = 2500, 1000, 20000
+    RUN = int(os.environ.get("C5STEPS", "400"))  # one persist_kernel launch integrates RUN steps
+    fetch = 2 * vf["FETCH_SIZE"] * 1024.0 / RUN
+    write = vw["WRITE_SIZE"] * 1024.0 / RUN
+    d = {"kernel": kf, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
+         "fetch_bytes_per_step": fetch, "write_bytes_per_step": write,
+         "fetch_bytes_per_launch": fetch * STEPS, "write_bytes_per_launch": write * STEPS,
+         "hbm_bytes_per_launch": (fetch + write) * STEPS, "dispatches": vf["dispatches"],
+         "state_bytes_per_step": B * N * 36, "connectome_bytes_per_step": 1024 * 1024 * 2 * 2,
+         "algorithmic_bytes_per_launch": B * N * (STEPS // 20 * 4 + 2 * 3 * 8 + 2 * 8),
+         "note": "rocprofv3 --pmc passes of `python3 tools/c5_pmc_run.py 400` (tools/profile_c5_pass.sh fetch / write): one persist_kernel "
+                 "dispatch of 400 Euler steps, divided by 400 and scaled by 20,000 to bench.py's per-chunk 'launch'. FETCH_SIZE x2 (gfx950), KB -> B; the "
+                 "counters include Infinity-Cache (MALL) hits; the state stays in registers, so the bytes are the "
+                 "per-step operand stream (connectome rows and the E image)."}
+    json.dump(d, open("profiles/pmc_sde_c5.json", "w"), indent=1)
+    print(json.dumps(d))
+
+
+def sq():
+    import json, sys
+    sys.path.insert(0, "tools")
+    from pmc_summary import summary
+    (ka, a), = summary("gpurun_out/prof_c5/sqa", "persist_kernel").items()
+    (_, b), = summary("gpurun_out/prof_c5/sqb", "persist_kernel").items()
+    STEPS, WAVES = 400, 256 * 8
+    act = a["GRBM_GUI_ACTIVE"] / 8 * 1024
+    d = {"kernel": ka, "steps": STEPS, "waves": WAVES,
+         "per_wave_step": {k: a[k] / (WAVES * STEPS) for k in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD")},
+         "salu_per_wave_step": b["SQ_INSTS_SALU"] / (WAVES * STEPS),
+         "mfma_busy_frac": a["SQ_VALU_MFMA_BUSY_CYCLES"] / act,
+         "valu_issue_busy_frac": 4 * a["SQ_ACTIVE_INST_VALU"] / act,
+         "lds_bank_conflict_frac": b["SQ_LDS_BANK_CONFLICT"] / max(1.0, b["SQ_LDS_IDX_ACTIVE"]),
+         "wave_cycle_split": {k: b[k] / b["SQ_WAVE_CYCLES"] for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS")},
+         "note": "rocprofv3 --pmc passes of tools/c5_pmc_run.py 400 (one persist_kernel dispatch of 400 Euler steps at the "
+                 "C5 shard, 2,500 x 1000, 8 waves per CU on 256 CUs). Busy fractions over GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs."}
+    json.dump(d, open("profiles/pmc_c5_sq.json", "w"), indent=1)
+    print(json.dumps(d))
+
+
+if __name__ == "__main__":
+    hbm()
+    sq()
