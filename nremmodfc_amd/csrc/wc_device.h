@@ -206,6 +206,21 @@ __device__ __forceinline__ void split2h(const float v[4], f16x4& hi, f16x4& lo) 
     }
 }
 
+// split2h of ONE pair (rows v[0], v[1]): the same operations as one iteration of split2h's loop,
+// the two fp16 halves packed in a dword each (hi, lo)
+template <bool PRE = false>
+__device__ __forceinline__ void split2h_pair(const float v[2], uint32_t& hi, uint32_t& lo) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const f2 x = PRE ? (f2){v[0], v[1]} : (f2){v[0], v[1]} * 1024.0f;
+    const h2 h = __builtin_convertvector(x, h2);
+    uint32_t lb;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lb) : "v"(x[0]), "v"(h));
+    asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lb) : "v"(x[1]), "v"(h));
+    hi = __builtin_bit_cast(uint32_t, h);
+    lo = lb;
+}
+
 // Plasticity variable a_ie: fp64, or a compensated fp32 pair (increments of
 // ~1e-6 on a ~2.5 are below fp32 half-ulp: plain fp32 would drop them).
 template <bool kPair> struct AccA;

@@ -240,6 +240,8 @@ enum : int {
     V_LEAN = 32768,   // packed fp32 update: a_ie as hi + lo running sum, renormalised every 16 steps
     V_AII0 = 65536,   // a_ii == 0 (host-checked): the inhibitory sigmoid without its in * cIi term
     V_ZMEM = 131072,  // the raw normals come precomputed from zbuf (zblock_kernel on otherwise idle CUs)
+    V_HALF2 = 262144, // NW = 2 NT: two waves per node tile, each updating two of a lane's four rows
+                      // (both run the tile's coupling MFMAs; with V_ZMEM, so no Philox is repeated)
 };
 
 constexpr bool kFragRegs_(int var) { return (var & V_FRAG_REGS) != 0; }
@@ -251,8 +253,10 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     typedef typename Tr<Real>::acc_t acc_t;
     typedef __attribute__((ext_vector_type(4))) Real real4;
     constexpr bool kMix = (VAR & V_MIX) != 0;
-    static_assert(kMix ? (NT == 6 && NW == 4) : NT % NW == 0, "NW must divide NT");
-    constexpr int OT = kMix ? 2 : NT / NW;  // tile slots per wave
+    constexpr bool kHalf = (VAR & V_HALF2) != 0;
+    static_assert(kMix ? (NT == 6 && NW == 4) : kHalf ? (NW == 2 * NT && SG == 1) : NT % NW == 0, "NW must divide NT");
+    constexpr int OT = kMix ? 2 : kHalf ? 1 : NT / NW;  // tile slots per wave
+    constexpr int RW = kHalf ? 2 : 4;                    // rows of a lane's 4 (one MFMA column quad) owned
     constexpr bool kHf = (VAR & V_F16X3) != 0;
     constexpr int kTerms = (VAR & V_BF16X6) ? 6 : (VAR & V_BF16X3) ? 3 : kHf ? 3 : 0;
     constexpr bool kBf = kTerms > 0;  // 16-bit split coupling (bf16 or fp16 parts)
@@ -275,6 +279,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr bool kLean = kFast && kPk && (VAR & V_LEAN) != 0;
     constexpr bool kAii0 = kFast && kPk && (VAR & V_AII0) != 0;
     constexpr bool kZMem = kFast && kPk && kRng && (VAR & V_ZMEM) != 0;
+    static_assert(!kHalf || (kZMem && kHf), "V_HALF2: the fp16x3 packed path with precomputed normals");
     constexpr float kEsc = kEs ? 1024.0f : 1.0f, kEinv = kEs ? 0x1p-10f : 1.0f;
     // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
     constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
@@ -311,7 +316,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     const int N = a.N;
     // this wave's tiles T0 .. T0 + nt - 1 (nt = OT except in V_MIX); a slot u >= nt maps to the
     // dead tile NT, whose nodes (>= 96 >= N) every n < N test skips
-    int T0 = NW == 1 ? 0 : w * OT, nt = OT;
+    int T0 = NW == 1 ? 0 : kHalf ? (w >> 1) : w * OT, nt = OT;
+    const int R0 = kHalf ? 2 * (w & 1) : 0;  // first owned row of the lane's four
     if constexpr (kMix) {
         static_assert(!kFragRegs_(VAR) && (VAR & V_ZFIRST) == 0, "V_MIX: LDS fragments, plain schedule");
         const int rot = grp & 3;
@@ -358,13 +364,13 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 
     // ---- own state and per-node parameters ----
     constexpr int PT = kParamRegs ? OT : 1;
-    Real E[OT][4], I[OT][4], Gc[PT][4], Sl[PT][4];
-    AccA<kPairA> A[OT][4];
+    Real E[OT][RW], I[OT][RW], Gc[PT][RW], Sl[PT][RW];
+    AccA<kPairA> A[OT][RW];
 #pragma unroll
     for (int u = 0; u < OT; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int n = 16 * TL(u) + 4 * g + r;
+        for (int r = 0; r < RW; ++r) {
+            const int n = 16 * TL(u) + 4 * g + R0 + r;
             const bool ok = n < N;
             const size_t o = (size_t)bb * N + (ok ? n : 0);
             E[u][r] = ok ? (Real)a.E[o] * (Real)kEsc : (Real)0;
@@ -406,7 +412,15 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     for (int r = 0; r < 4; ++r) X[t][r] = E[t][r];
             }
         } else {
-            if constexpr (kBf) {
+            if constexpr (kHalf) {
+                // the owned two rows: one dword (two fp16) of the tile's 8-B slot per part
+                uint32_t* x2 = reinterpret_cast<uint32_t*>(xb16 + buf * NC * PS * 64);
+                const int t = TL(0);
+                uint32_t hl[2];
+                split2h_pair<kEs>(E[0], hl[0], hl[1]);
+#pragma unroll
+                for (int p = 0; p < 2; ++p) x2[((((t >> 1) * PS + p) * 64 + lane) * 2 + (t & 1)) * 2 + (R0 >> 1)] = hl[p];
+            } else if constexpr (kBf) {
                 bf16x4* x4 = reinterpret_cast<bf16x4*>(xb16 + buf * NC * PS * 64);
 #pragma unroll
                 for (int u = 0; u < OT; ++u) {
@@ -454,17 +468,22 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     int rec_cnt = 0, rec_row = 0;
     // record buffer (RB > 1): the RB-1 previous E records of this lane's nodes, oldest first
     constexpr int RB = (VAR & V_REC4) ? 4 : (VAR & V_REC2) ? 2 : 1;
-    Real rbuf[RB > 1 ? OT : 1][4][RB > 1 ? RB - 1 : 1];
+    Real rbuf[RB > 1 ? OT : 1][RW][RB > 1 ? RB - 1 : 1];
 
     // V_ZMEM: normals of the next kZD steps in flight
     constexpr int kZD = kZMem ? 4 : 1;
-    float4 zq[kZD][kZMem ? OT : 1];
+    typedef std::conditional_t<kHalf, float2, float4> zt;  // V_HALF2: the owned rows' two normals
+    auto zload = [&](int st_, int u) -> zt {
+        const size_t q = (((size_t)st_ * NT + TL(u)) * a.zBp + (size_t)b) * 4 + g;
+        if constexpr (kHalf) return reinterpret_cast<const float2*>(a.zbuf)[q * 2 + (R0 >> 1)];
+        else return a.zbuf[q];
+    };
+    zt zq[kZD][kZMem ? OT : 1];
     if constexpr (kZMem) {
 #pragma unroll
         for (int d = 0; d < kZD; ++d)
 #pragma unroll
-            for (int u = 0; u < OT; ++u)
-                zq[d][u] = a.zbuf[(((size_t)min(d, a.nsteps - 1) * NT + TL(u)) * a.zBp + (size_t)b) * 4 + g];
+            for (int u = 0; u < OT; ++u) zq[d][u] = zload(min(d, a.nsteps - 1), u);
     }
     // one Euler step; ZS = the V_ZMEM prefetch slot of step s (s % kZD: a compile-time index, so the
     // in-flight normals are never moved between registers -- a move would wait for every older load)
@@ -481,8 +500,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                             for (int u = 0; u < OT; ++u)
 #pragma unroll
-                                for (int r = 0; r < 4; ++r) {
-                                    const int n = 16 * TL(u) + 4 * g + r;
+                                for (int r = 0; r < RW; ++r) {
+                                    const int n = 16 * TL(u) + 4 * g + R0 + r;
                                     if (n < N) {
                                         Real* dst = static_cast<Real*>(a.recE) + ((size_t)bb * N + n) * a.rec_ld +
                                                     (rec_row - (RB - 1));
@@ -500,7 +519,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                         for (int u = 0; u < OT; ++u)
 #pragma unroll
-                            for (int r = 0; r < 4; ++r) {
+                            for (int r = 0; r < RW; ++r) {
 #pragma unroll
                                 for (int k = 0; k + 1 < RB - 1; ++k) rbuf[u][r][k] = rbuf[u][r][k + 1];
                                 rbuf[u][r][RB - 2] = E[u][r] * (Real)kEinv;
@@ -510,8 +529,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                     for (int u = 0; u < OT; ++u)
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int n = 16 * TL(u) + 4 * g + r;
+                        for (int r = 0; r < RW; ++r) {
+                            const int n = 16 * TL(u) + 4 * g + R0 + r;
                             if (n < N) {
                                 const size_t cc = (size_t)bb * N + n;
                                 const size_t o = a.rec_ld ? cc * a.rec_ld + rec_row : (size_t)rec_row * BN + cc;
@@ -536,13 +555,13 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         const uint64_t gstep = (uint64_t)(a.step0 + s);
         // V_ZMEM: this step's normals were loaded kZD steps ago (a step is shorter than a memory
         // round trip); issue the load of step s + kZD now (clamped to the block's last step)
-        float4 zm[kZMem ? OT : 1];
+        zt zm[kZMem ? OT : 1];
         if constexpr (kZMem) {
             const int sl = min(s + kZD, a.nsteps - 1);
 #pragma unroll
             for (int u = 0; u < OT; ++u) {
                 zm[u] = zq[ZS][u];
-                zq[ZS][u] = a.zbuf[(((size_t)sl * NT + TL(u)) * a.zBp + (size_t)b) * 4 + g];
+                zq[ZS][u] = zload(sl, u);
             }
         }
         // V_ZFIRST: the normals do not depend on the coupling, so they can fill the MFMA chain's gaps
@@ -630,7 +649,23 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             if (!owned(u)) continue;
             if constexpr (sizeof(Real) == 8) __builtin_amdgcn_sched_barrier(0);  // fp64: bound live ranges
             Real z[4] = {0, 0, 0, 0};
-            if constexpr (kFast && kPk) {
+            if constexpr (kHalf) {
+                // the owned pair (rows R0, R0 + 1): pair R0 / 2 of the full-tile form, same operations
+                f2v e = {E[u][0], E[u][1]}, in = {I[u][0], I[u][1]};
+                f2v ahi = {A[u][0].hi, A[u][1].hi}, alo = {A[u][0].lo, A[u][1].lo};
+                const f2v cpl = R0 ? f2v{acc[u][2], acc[u][3]} : f2v{acc[u][0], acc[u][1]};
+                cell_pair_f32<kEs, kLean, kAii0>(pk, e, in, ahi, alo, cpl, f2v{Gc[u][0], Gc[u][1]},
+                                                  f2v{Sl[u][0], Sl[u][1]}, f2v{zm[u].x, zm[u].y});
+                E[u][0] = e.x;
+                E[u][1] = e.y;
+                I[u][0] = in.x;
+                I[u][1] = in.y;
+                A[u][0].hi = ahi.x;
+                A[u][1].hi = ahi.y;
+                A[u][0].lo = alo.x;
+                A[u][1].lo = alo.y;
+                continue;
+            } else if constexpr (kFast && kPk) {
                 f2v zp[2] = {f2v{0, 0}, f2v{0, 0}};
                 if constexpr (kZMem) {
                     zp[0] = f2v{zm[u].x, zm[u].y};
@@ -660,7 +695,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 }
                 continue;
             }
-            if constexpr (kFast) {
+            if constexpr (kFast && !kHalf) {
                 if constexpr (kZFirst) {
 #pragma unroll
                     for (int r = 0; r < 4; ++r) z[r] = zz[u][r];
@@ -693,6 +728,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 }
                 continue;
             }
+            if constexpr (!kHalf) {
             if constexpr (kRng) quad_normals(gstep, (uint32_t)(4 * TL(u) + g), key, z);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -726,13 +762,14 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     A[u][r].add(dtA * (in * (e - rhoE)));
                 }
             }
+            }  // !kHalf
         }
         if constexpr (kLean) {
             if ((s & 15) == 15) {  // fold the running increments into hi (wave-uniform branch)
 #pragma unroll
                 for (int u = 0; u < OT; ++u)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
+                    for (int r = 0; r < RW; ++r) {
                         const float hs = A[u][r].hi + A[u][r].lo;
                         A[u][r].lo = A[u][r].lo - (hs - A[u][r].hi);
                         A[u][r].hi = hs;
@@ -764,8 +801,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
             for (int u = 0; u < OT; ++u)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int n = 16 * TL(u) + 4 * g + r;
+                for (int r = 0; r < RW; ++r) {
+                    const int n = 16 * TL(u) + 4 * g + R0 + r;
                     if (n < N) {
                         Real* dst = static_cast<Real*>(a.recE) + ((size_t)bb * N + n) * a.rec_ld + (rec_row - m);
 #pragma unroll
@@ -780,8 +817,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
         for (int u = 0; u < OT; ++u)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int n = 16 * TL(u) + 4 * g + r;
+            for (int r = 0; r < RW; ++r) {
+                const int n = 16 * TL(u) + 4 * g + R0 + r;
                 if (n < N) {
                     const size_t o = (size_t)b * N + n;
                     a.E[o] = (double)(E[u][r] * (Real)kEinv);
@@ -886,6 +923,10 @@ size_t zmem_offset(int N) { return (frag_bytes(N, WC_F32) + 255) / 256 * 256; }
 // of a tile's step.  Each launch covers kZK steps with one workgroup per CU: the integrating
 // workgroups read this block's normals from a buffer, the others draw the next block's
 // (double-buffered, ordered by the launches on one stream; launch_zmem).
+#ifndef WC_ZMEM_HALF
+#define WC_ZMEM_HALF 1  // the normals-block path runs 12 waves per group, half a node tile each (V_HALF2;
+                        // 0: six waves of one tile, 2,500 sims 0.747 vs 0.708 us per step, profiles/r03_half_ab.log)
+#endif
 constexpr int kZK = 1000;                // steps per launch (a multiple of the drivers' rec_every 20)
 constexpr int kZMinIdle = 32;            // CUs the generator needs at least
 constexpr int kZMaxGroups = 160;         // measured regime: up to 2,560 simulations (the 8-way C3 shard)
@@ -951,7 +992,11 @@ int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int
             if (ka.recI) kb.recI = static_cast<float*>(ka.recI) + off;
             if (ka.recA) kb.recA = static_cast<float*>(ka.recA) + off;
         }
+#if WC_ZMEM_HALF
+        const int rc = launch_v<float, 6, 12, kVarF32 | X | V_ZMEM | V_HALF2>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);
+#else
         const int rc = launch_v<float, 6, 6, kVarF32 | X | V_ZMEM>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);
+#endif
         if (rc != WC_OK) return rc;
     }
     return wc_hip_check("wc_integrate (normals-block path)");
