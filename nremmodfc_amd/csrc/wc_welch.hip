@@ -377,7 +377,12 @@ __device__ __forceinline__ void wstage1(f2* z, f2 (&x)[7][5], const f2* __restri
         for (int r = 0; r < 5; ++r) {
             part += R::own(lane, q) ? x[q][r].x + x[q][r].y : 0.f;
             // (w(2m), w(2m+1)); unsigned byte offset: the saddr form of the load
+#if defined(WC_WELCH_DIAG_NOHANN)  // (ablation builds only: timing without the window loads, wrong PSD)
+            hw[q][r] = (f2){1.0f, 1.0f};
+            (void)i;
+#else
             hw[q][r] = *reinterpret_cast<const f2*>(reinterpret_cast<const char*>(hann) + (unsigned)(i + r * R::S) * 8u);
+#endif
         }
     }
     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
