@@ -300,12 +300,16 @@ def test_f32_nonzero_a_ii(cuda, sc90, B):
     assert mx <= 2e-6 and rms <= 3e-7, (mx, rms)
 
 
-@pytest.mark.parametrize("B,nsteps,ring", [(2500, 2400, False), (161, 4100, True), (37, 2020, False)])
-def test_small_batch_precomputed_normals_bit_identical(cuda, sc90, B, nsteps, ring, monkeypatch):
-    """Small batches (strong-scaling shards) draw their normals in blocks on the idle CUs (V_ZMEM,
-    CU-masked streams, double-buffered); the trajectory, every record (time-major or the pipeline's
-    node-major ring) and the final state equal the in-kernel-noise kernel's bit for bit, including a
-    short last block."""
+@pytest.mark.parametrize("N,B,nsteps,ring", [(90, 2500, 2400, False), (90, 161, 4100, True), (90, 37, 2020, False),
+                                             (81, 203, 2040, True), (96, 130, 2100, False)])
+def test_small_batch_precomputed_normals_bit_identical(cuda, sc90, N, B, nsteps, ring, monkeypatch):
+    """Small batches (strong-scaling shards) draw their normals in blocks on the idle CUs of the same
+    launch (V_ZMEM) and run twelve waves per group, half a node tile each (V_HALF2); the trajectory,
+    every record (time-major or the pipeline's node-major ring) and the final state equal the
+    in-kernel-noise six-wave kernel's bit for bit, including a short last block and the ragged node
+    counts of the six-tile range (81: the last tile's rows past N masked in both halves)."""
+    from nremmodfc_amd import datasets
+    sc = sc90 if N == 90 else datasets.synthetic_sc(N)
     rng = np.random.default_rng(B)
     G = 0.16 + rng.uniform(-0.1, 0.3, B)
     S = 7.68 + rng.uniform(-0.2, 0.2, B)
@@ -314,16 +318,17 @@ def test_small_batch_precomputed_normals_bit_identical(cuda, sc90, B, nsteps, ri
     out = {}
     for zm in ("1", "0"):
         monkeypatch.setenv("WCSDE_ZMEM", zm)
-        bt = Batch(sc90, G, S, keys, precision="f32")
+        bt = Batch(sc, G, S, keys, precision="f32")
         bt.integrate(100, 0.05)
         if ring:
             ld = n_rec + 3
-            rec = torch.full((B * 90 * ld,), float("nan"), dtype=torch.float32, device="cuda")
+            rec = torch.full((B * N * ld,), float("nan"), dtype=torch.float32, device="cuda")
             bt.integrate(nsteps, 2.0, 20, rec, rec_ld=ld)
         else:
-            rec = torch.empty((n_rec, B, 90), dtype=torch.float32, device="cuda")
+            rec = torch.empty((n_rec, B, N), dtype=torch.float32, device="cuda")
             bt.integrate(nsteps, 2.0, 20, rec)
         torch.cuda.synchronize()
         out[zm] = (rec, bt.E, bt.I, bt.A)
+    assert torch.isfinite(out["1"][1]).all()
     for a, b in zip(out["1"], out["0"]):
         assert torch.equal(torch.nan_to_num(a, nan=-1.0), torch.nan_to_num(b, nan=-1.0))
