@@ -8,8 +8,8 @@ dG, sigmaE = 7.68 + dsigma on the shipped grid (whole_sweep_both_maps.py:92-93).
 One bench "step" = 2000 recorded samples of every simulation of the batch: two
 chunks of 20,000 Euler steps of the recorded phase (tau_ip = 2, E stored every
 20 steps, wc:118-135), each followed by the streamed BOLD / band-pass stage
-(which also transposes the chunk into the 4-slot Welch ring), plus one
-4000-sample Welch segment -- the steady state of
+(which also transposes the chunk into the 6-slot Welch ring), plus one
+4000-sample Welch segment (a launch of the last two every other step) -- the steady state of
 the sweep pipeline (nremmodfc_amd/pipeline.py); inputs and state resident in
 HBM.  --sde-only times the integrator alone.  With --gpus N (torchrun, one rank per
 GPU) each rank runs its own 20,000-simulation shard (seeds 50r..50r+49):
@@ -199,10 +199,11 @@ def main():
     p = driver_params()
     dev = torch.device("cuda", local)
     bt = Batch(sc, G, S, keys, p, precision=args.precision, device=dev)
-    R, CH, NSLOT = 20, 1000, 4           # record every 20 steps; 1000-sample chunks; 4-slot ring
+    R, CH, NSLOT = 20, 1000, 6           # record every 20 steps; 1000-sample chunks; 6-slot ring (Welch pairs)
     LD = CH * NSLOT
     EULER = CH * R                       # Euler steps per chunk
-    CHUNKS = 2                           # chunks per bench step (one Welch segment per step)
+    CHUNKS = 2                           # chunks per bench step (one Welch segment per step: a launch of two
+                                         # overlapping segments every other step, as the sweep pipeline runs them)
     n_total = (args.warmup + args.steps) * CHUNKS * CH + NEQ
     ring = torch.empty(C * LD, dtype=bt.rec_dtype, device=dev)
     # fp32 + consumers: the integrator writes each chunk time-major, the BOLD pass transposes it
@@ -229,7 +230,8 @@ def main():
 
     def step():
         """2000 recorded samples (40,000 Euler steps) of every simulation: integrate into the ring,
-        stream BOLD over each 1000-sample chunk, one 4000-sample Welch segment."""
+        stream BOLD over each 1000-sample chunk, one 4000-sample Welch segment (every other step one
+        launch of the last two segments, as nremmodfc_amd/pipeline.py does)."""
         for _ in range(CHUNKS):
             k = state["k"]
             slot = k % NSLOT
@@ -241,8 +243,8 @@ def main():
                 if bold is not None:
                     timed("bold", lambda: bold.feed(ring, CH, e_ld=LD, offset=slot * CH))
             state["k"] = k = k + 1
-            if welch is not None and k >= NSLOT and k % 2 == 0:
-                timed("welch", lambda: welch.accumulate(ring, LD, CH, NSLOT, (k - NSLOT) * CH))
+            if welch is not None and k >= NSLOT and k % 4 == 2:
+                timed("welch", lambda: welch.accumulate(ring, LD, CH, NSLOT, (k - NSLOT) * CH, nseg=2))
 
     for _ in range(args.warmup):
         step()
@@ -264,6 +266,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern = {k: (sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None) for k, v in ev.items()}
+    if kern["welch"] is not None:
+        kern["welch"] /= 2  # ms per segment (each launch takes two)
     B_all = B
     if dist:  # strong scaling: shards may differ by one simulation
         t = torch.tensor([B], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.int64)

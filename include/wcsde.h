@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define WCSDE_ABI_VERSION 5
+#define WCSDE_ABI_VERSION 6
 
 /* Noise stream (the reference's numba RNG is seeded from os.urandom and never
  * reproducible; the build defines its own): Philox4x32-10 with
@@ -266,8 +266,9 @@ int wc_kuramoto(int B, int N, int M, const double* phasor, double* out, void* st
 /* ------------------------------------------------------------------------
  * Welch peak frequency (whole_sweep_both.py:90-95): signal.welch(E_t.T, fs,
  * nperseg=4000), node-mean PSD, first argmax.  wc_welch_prepare fills the
- * twiddle workspace once; wc_welch_accumulate adds one segment
- * [seg0, seg0+4000) of every column to acc [B][2001] (fp64, zero it first);
+ * twiddle workspace once; wc_welch_accumulate adds nseg (1 or 2) consecutive segments
+ * [seg0 + 2000 k, seg0 + 2000 k + 4000), k < nseg, of every column to acc [B][2001] (fp64, zero it
+ * first; the ring must hold the nseg segments' span, 4000 or 6000 samples);
  * E is node-major: sample t of column c at
  *   c*ld + ((t / slot) % nslots) * slot + t % slot   (a ring of nslots slots);
  * wc_welch_peak turns acc (nseg segments) into peak [B] (Hz) and optionally
@@ -276,7 +277,8 @@ size_t wc_welch_workspace_size(void);
 int wc_welch_bins(void);
 int wc_welch_prepare(void* workspace, size_t ws_bytes, void* stream);
 int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int64_t slot,
-                        int64_t nslots, int64_t seg0, const void* workspace, double* acc, void* stream);
+                        int64_t nslots, int64_t seg0, int nseg, const void* workspace, double* acc,
+                        void* stream);
 int wc_welch_peak(int B, int N, int nseg, double fs, const double* acc, double* peak, double* psd,
                   void* stream);
 

@@ -76,7 +76,7 @@ _SIGNATURES = {
     "wc_welch_workspace_size": (c_sz, []),
     "wc_welch_bins": (c_int, []),
     "wc_welch_prepare": (c_int, [c_vp, c_sz, c_vp]),
-    "wc_welch_accumulate": (c_int, [c_int, c_int, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "wc_welch_accumulate": (c_int, [c_int, c_int, c_vp, c_int, c_i64, c_i64, c_i64, c_i64, c_int, c_vp, c_vp, c_vp]),
     "wc_welch_peak": (c_int, [c_int, c_int, c_int, c_dbl, c_vp, c_vp, c_vp, c_vp]),
 }
 

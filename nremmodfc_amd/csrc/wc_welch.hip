@@ -124,7 +124,8 @@ struct WelchArgs {
     int B, N;
     const void* E;     // node-major ring: element (c, t) at c*ld + ((t/slot) % nslots)*slot + t % slot
     int64_t ld, slot, nslots;
-    int64_t seg0;      // first sample of the segment
+    int64_t seg0;      // first sample of the (first) segment
+    int nseg;          // consecutive segments (hop kSeg / 2) in this launch: 1 or 2 (welch_wave_kernel)
     const double* tw;  // twiddle table
     double* acc;       // [B][kBins] running sum over nodes and segments of |X_k|^2
 };
@@ -518,6 +519,9 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
     // saddr form, an SGPR base plus a 32-bit lane offset, instead of a 64-bit VGPR address each)
     const int wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int w = wg & (kWv - 1);                         // column slot within the simulation
+    // nseg == 2: waves w and w ^ 1 take segments 0 and 1 of the same column at the same time (the
+    // half they share is read once from HBM, once from the caches), each wave every other column
+    const int sgi = w % a.nseg, cstep = kWv / a.nseg, c0 = w / a.nseg;
     const int b = blockIdx.x * kSimsWg + wg / kWv;        // this wave's simulation
     const int ncol = b < a.B ? a.N : 0;
     f2* z = reinterpret_cast<f2*>(smem) + wg * kFFT;
@@ -532,7 +536,7 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
     // the ring is circular per column: sample seg0 + t sits at (seg0 + t) mod L, L = slot * nslots
     // (byte offsets in 32 bits: the host admits ld < INT32_MAX / 2 - 8192, so 4 (L + 4000) < 2^32)
     const unsigned L = (unsigned)(a.slot * a.nslots);
-    const unsigned baseB = (unsigned)(a.seg0 % L) * 4u, LB = L * 4u;
+    const unsigned baseB = (unsigned)((a.seg0 + (int64_t)sgi * (kSeg / 2)) % L) * 4u, LB = L * 4u;
     // stage-1 inputs come straight from HBM into registers, in the butterfly layout
     // (x[q][r] = packed point i + 400 r, i = lane + 64 q); the next column is fetched
     // while the current one is transformed (branch-free: the clamped lanes of row 6
@@ -552,7 +556,7 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
             }                                                                                  \
         }                                                                                      \
     }
-    WELCH_FETCH(min(w, a.N - 1), 0, 7, lane);
+    WELCH_FETCH(min(c0, a.N - 1), 0, 7, lane);
     {  // twiddle tables into LDS: T^0..T^2000 and the stage tables (the pad entry is never read)
         const f2* src = reinterpret_cast<const f2*>(twg);
         const f2* sst = reinterpret_cast<const f2*>(twg) + kSeg + kFFT;
@@ -561,7 +565,7 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
     }
     __syncthreads();
 
-    for (int n = w; n < ncol; n += kWv) {
+    for (int n = c0; n < ncol; n += cstep) {
         // (the lane id is laundered per column so the compiler does not hoist hundreds
         // of loop-invariant twiddle offsets out of the column loop)
         int ln = lane;
@@ -571,7 +575,7 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
         //      the real-FFT unpack into the last ----
         wstage1(z, x, hann, ln);
         // the Hann loads have retired: the next column's loads are the only VMEM in flight
-        const int nn = n + kWv < ncol ? n + kWv : n;
+        const int nn = n + cstep < ncol ? n + cstep : n;
 #if defined(WC_WELCH_DIAG_NOLOAD)  // (ablation builds only: tools/dbg/welch_variants.sh)
         (void)nn;
 #else
@@ -909,22 +913,27 @@ int wc_welch_prepare(void* workspace, size_t ws_bytes, void* stream) {
 }
 
 int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int64_t slot, int64_t nslots,
-                        int64_t seg0, const void* workspace, double* acc, void* stream) {
+                        int64_t seg0, int nseg, const void* workspace, double* acc, void* stream) {
     wc_clear_err();
     if (B <= 0 || N <= 0 || !E || !acc || !workspace || slot <= 0 || nslots <= 0 || seg0 < 0 || ld < slot * nslots ||
-        kSeg > slot * nslots)
+        nseg < 1 || nseg > 2 || kSeg + (int64_t)(nseg - 1) * (kSeg / 2) > slot * nslots)
         return wc_set_err(WC_EINVAL, "wc_welch_accumulate: bad arguments");
-    WelchArgs a{B, N, E, ld, slot, nslots, seg0, static_cast<const double*>(workspace), acc};
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (e_f64) {
-        const size_t lds = (size_t)2 * kG<double> * kFFT * sizeof(cx<double>) + 4 * kG<double> * sizeof(double);
-        hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<double>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
-        hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
-    } else {
-        if (ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 && ld < INT32_MAX / 2 - 8192) {
+    const bool wave = !e_f64 && ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 &&
+                      ld < INT32_MAX / 2 - 8192;
+    // the LDS-Stockham kernels (fp64 input, unaligned rings) take one segment per launch
+    for (int sg = 0; sg < (wave ? 1 : nseg); ++sg) {
+        WelchArgs a{B, N, E, ld, slot, nslots, seg0 + (int64_t)sg * (kSeg / 2), wave ? nseg : 1,
+                    static_cast<const double*>(workspace), acc};
+        if (e_f64) {
+            const size_t lds = (size_t)2 * kG<double> * kFFT * sizeof(cx<double>) + 4 * kG<double> * sizeof(double);
+            hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<double>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
+            hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
+        } else if (wave) {
 #if WC_WELCH_PAIR
+            if (nseg != 1) return wc_set_err(WC_EINVAL, "wc_welch_accumulate: the pair build takes one segment");
             hipError_t ea = hipFuncSetAttribute((const void*)welch_pair_kernel,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPairLds);
             if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));

@@ -14,9 +14,10 @@ do one simulation at a time:
 The recorded phase runs in chunks of `chunk_samples` samples (20 Euler steps
 each).  The integrator writes each chunk time-major ([chunk][C] fp32, 7.2 GB
 at 20,000 x 90: full-line stores); the BOLD stream consumes it right away and
-in the same pass writes it node-major into one slot of a 4-slot ring ([C][4*chunk]
-fp32, 28.8 GB), from which every completed 4000-sample Welch segment is
-transformed -- the 648 MB/simulation trajectory of the reference never exists.
+in the same pass writes it node-major into one slot of a 6-slot ring ([C][6*chunk]
+fp32, 43.2 GB), from which the completed 4000-sample Welch segments are
+transformed two at a time (one launch reads their shared half once from HBM) --
+the 648 MB/simulation trajectory of the reference never exists.
 """
 from __future__ import annotations
 
@@ -100,7 +101,9 @@ def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedul
             if progress:
                 progress("transient", bt.step, sch.n_total)
     # ---- recorded phase, streamed ----
-    nslots = WELCH_NPERSEG // chunk_samples
+    # a 6000-sample ring: Welch takes its segments two at a time (one launch reads their shared
+    # half once from HBM), the last one alone if the count is odd
+    nslots = (WELCH_NPERSEG + WELCH_HOP) // chunk_samples
     ld = nslots * chunk_samples
     ring = torch.empty(C * ld, dtype=bt.rec_dtype, device=bt.device)
     # fp32: the integrator writes each chunk time-major (full-line stores) and the BOLD
@@ -120,11 +123,14 @@ def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedul
             bold.feed(ring, n_samp, e_ld=ld, offset=slot * chunk_samples)
         t_done += n_samp
         k += 1
-        while welch is not None and next_seg * WELCH_HOP + WELCH_NPERSEG <= t_done:
-            welch.accumulate(ring, ld, chunk_samples, nslots, next_seg * WELCH_HOP)
-            next_seg += 1
+        while welch is not None and next_seg * WELCH_HOP + WELCH_NPERSEG + WELCH_HOP <= t_done:
+            welch.accumulate(ring, ld, chunk_samples, nslots, next_seg * WELCH_HOP, nseg=2)
+            next_seg += 2
         if progress:
             progress("recorded", bt.step, sch.n_total)
+    if welch is not None and next_seg * WELCH_HOP + WELCH_NPERSEG <= T:  # an odd last segment (still in the ring)
+        welch.accumulate(ring, ld, chunk_samples, nslots, next_seg * WELCH_HOP)
+        next_seg += 1
     torch.cuda.synchronize(bt.device)  # the phase timings below are of finished work, not queued launches
     t_sde = time.perf_counter()
     # ---- epilogue ----

@@ -194,13 +194,14 @@ class WelchAccumulator:
         self.acc = torch.zeros((B, self.bins), dtype=torch.float64, device=self.device)
         self.nseg = 0
 
-    def accumulate(self, E, ld, slot, nslots, seg0):
-        """Add segment [seg0, seg0+4000) of every column of the node-major ring E."""
+    def accumulate(self, E, ld, slot, nslots, seg0, nseg=1):
+        """Add segments [seg0 + 2000 k, seg0 + 2000 k + 4000), k < nseg (1 or 2), of every column of the
+        node-major ring E (two in one launch read their shared half once from HBM)."""
         f64 = E.dtype == torch.float64
-        rc = _lib.lib().wc_welch_accumulate(self.B, self.N, _ptr_at(E), int(f64), ld, slot, nslots, seg0,
+        rc = _lib.lib().wc_welch_accumulate(self.B, self.N, _ptr_at(E), int(f64), ld, slot, nslots, seg0, nseg,
                                             _lib.ptr(self.ws), _lib.ptr(self.acc), _lib.stream_handle())
         _lib.check(rc, "wc_welch_accumulate")
-        self.nseg += 1
+        self.nseg += nseg
 
     def peak(self, fs=500.0, want_psd=False):
         peak = torch.empty(self.B, dtype=torch.float64, device=self.device)

@@ -39,7 +39,7 @@ def test_product_library_has_no_diagnostic_entry_points():
 def test_abi_version_and_workspace():
     from nremmodfc_amd import _lib
     L = _lib.lib()
-    assert L.wcsde_abi_version() == 5
+    assert L.wcsde_abi_version() == 6
     # N <= 96: sized for the 3-part 16-bit image (the fp16x2 image and its two scale floats fit inside)
     assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16
     assert L.wc_workspace_size(20000, 90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8

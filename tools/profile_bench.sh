@@ -58,7 +58,7 @@ sig = {"note": "rocprofv3 --pmc passes of the same bench run (tools/profile_benc
                "SQ_ACTIVE_INST_ANY (issuing), fractions of SQ_WAVE_CYCLES."}
 C = 20000 * 90
 for name, sub, units, per in (("bold_steady_copy", "bold_chunk_kernel<float, true, true, true>", C * 1000.0 / 64, "wave-sample"),
-                              ("welch", "welch_wave_kernel", float(C), "column-segment")):
+                              ("welch", "welch_wave_kernel", 2.0 * C, "column-segment")):  # (two segments per launch)
     a = summary("gpurun_out/prof/sq", sub)
     b = summary("gpurun_out/prof/sq2", sub)
     fe = summary("gpurun_out/prof/fetch", sub)
