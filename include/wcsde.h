@@ -266,9 +266,9 @@ int wc_kuramoto(int B, int N, int M, const double* phasor, double* out, void* st
 /* ------------------------------------------------------------------------
  * Welch peak frequency (whole_sweep_both.py:90-95): signal.welch(E_t.T, fs,
  * nperseg=4000), node-mean PSD, first argmax.  wc_welch_prepare fills the
- * twiddle workspace once; wc_welch_accumulate adds nseg (1 or 2) consecutive segments
+ * twiddle workspace once; wc_welch_accumulate adds nseg (1, 2 or 4) consecutive segments
  * [seg0 + 2000 k, seg0 + 2000 k + 4000), k < nseg, of every column to acc [B][2001] (fp64, zero it
- * first; the ring must hold the nseg segments' span, 4000 or 6000 samples);
+ * first; the ring must hold the nseg segments' span, 4000 + 2000 (nseg - 1) samples);
  * E is node-major: sample t of column c at
  *   c*ld + ((t / slot) % nslots) * slot + t % slot   (a ring of nslots slots);
  * wc_welch_peak turns acc (nseg segments) into peak [B] (Hz) and optionally

@@ -125,7 +125,7 @@ struct WelchArgs {
     const void* E;     // node-major ring: element (c, t) at c*ld + ((t/slot) % nslots)*slot + t % slot
     int64_t ld, slot, nslots;
     int64_t seg0;      // first sample of the (first) segment
-    int nseg;          // consecutive segments (hop kSeg / 2) in this launch: 1 or 2 (welch_wave_kernel)
+    int nseg;          // consecutive segments (hop kSeg / 2) in this launch: 1, 2 or 4 (welch_wave_kernel)
     const double* tw;  // twiddle table
     double* acc;       // [B][kBins] running sum over nodes and segments of |X_k|^2
 };
@@ -520,7 +520,8 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
     const int wg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int w = wg & (kWv - 1);                         // column slot within the simulation
     // nseg == 2: waves w and w ^ 1 take segments 0 and 1 of the same column at the same time (the
-    // half they share is read once from HBM, once from the caches), each wave every other column
+    // half they share is read once from HBM, once from the caches), each wave every other column;
+    // nseg == 4: wave w takes segment w of every column
     const int sgi = w % a.nseg, cstep = kWv / a.nseg, c0 = w / a.nseg;
     const int b = blockIdx.x * kSimsWg + wg / kWv;        // this wave's simulation
     const int ncol = b < a.B ? a.N : 0;
@@ -916,7 +917,7 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
                         int64_t seg0, int nseg, const void* workspace, double* acc, void* stream) {
     wc_clear_err();
     if (B <= 0 || N <= 0 || !E || !acc || !workspace || slot <= 0 || nslots <= 0 || seg0 < 0 || ld < slot * nslots ||
-        nseg < 1 || nseg > 2 || kSeg + (int64_t)(nseg - 1) * (kSeg / 2) > slot * nslots)
+        (nseg != 1 && nseg != 2 && nseg != 4) || kSeg + (int64_t)(nseg - 1) * (kSeg / 2) > slot * nslots)
         return wc_set_err(WC_EINVAL, "wc_welch_accumulate: bad arguments");
     hipStream_t st = static_cast<hipStream_t>(stream);
     const bool wave = !e_f64 && ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 &&

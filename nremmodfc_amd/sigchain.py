@@ -195,8 +195,8 @@ class WelchAccumulator:
         self.nseg = 0
 
     def accumulate(self, E, ld, slot, nslots, seg0, nseg=1):
-        """Add segments [seg0 + 2000 k, seg0 + 2000 k + 4000), k < nseg (1 or 2), of every column of the
-        node-major ring E (two in one launch read their shared half once from HBM)."""
+        """Add segments [seg0 + 2000 k, seg0 + 2000 k + 4000), k < nseg (1, 2 or 4), of every column of
+        the node-major ring E (segments in one launch read their shared halves once from HBM)."""
         f64 = E.dtype == torch.float64
         rc = _lib.lib().wc_welch_accumulate(self.B, self.N, _ptr_at(E), int(f64), ld, slot, nslots, seg0, nseg,
                                             _lib.ptr(self.ws), _lib.ptr(self.acc), _lib.stream_handle())

@@ -166,25 +166,28 @@ def test_welch_f32_ring_wrap_and_small_n(cuda, B, N):
         np.testing.assert_allclose(psd[b].cpu().numpy(), mp, rtol=2e-4, atol=2e-4 * mp.max())
 
 
-@pytest.mark.parametrize("B,N", [(5, 1), (3, 2), (4, 9), (2, 90)])
-def test_welch_f32_two_segments_per_launch(cuda, B, N):
-    """nseg = 2 (the pipeline's form): one launch of two overlapping segments over a 6-slot ring,
-    wrapping, equals the two segments launched one by one to fp32 summation order (the waves
-    group the per-lane sums differently), with the same peaks; and the PSD matches the oracle.
-    N < 2 leaves the second segment's waves of a column idle."""
-    T = 10000
+@pytest.mark.parametrize("B,N,K", [(5, 1, 2), (3, 2, 2), (4, 9, 2), (2, 90, 2), (3, 3, 4), (2, 90, 4)])
+def test_welch_f32_two_segments_per_launch(cuda, B, N, K):
+    """nseg = K (2: the pipeline's form; 4): one launch of K overlapping segments over a ring of
+    4000 + 2000 (K - 1) samples, wrapping, equals the K segments launched one by one to fp32
+    summation order (the waves group the per-lane sums differently), with the same peaks; and the
+    PSD matches the oracle.  Small N leaves some waves of a simulation idle."""
+    span = 4000 + 2000 * (K - 1)
+    T = 4000 + span
     X = torch.from_numpy(_e_like(T, B * N, B * 20 + N).T.copy()).to("cuda", torch.float32)  # [C][T]
-    slot, nslots, ld = 1000, 6, 6144
+    slot = 1000
+    nslots = span // slot
+    ld = nslots * slot + 144
     ring = torch.zeros((B * N, ld), dtype=torch.float32, device="cuda")
-    for t0 in range(4000, T, slot):  # samples [4000, 10000) into slots (t // slot) % 6
+    for t0 in range(4000, T, slot):  # samples [4000, T) into slots (t // slot) % nslots
         q = (t0 // slot) % nslots
         ring[:, q * slot:(q + 1) * slot] = X[:, t0:t0 + slot]
     two = wsg.WelchAccumulator(B, N)
-    two.accumulate(ring.reshape(-1), ld, slot, nslots, 4000, nseg=2)  # [4000, 8000) and [6000, 10000)
+    two.accumulate(ring.reshape(-1), ld, slot, nslots, 4000, nseg=K)  # [4000 + 2000 k, 8000 + 2000 k)
     one = wsg.WelchAccumulator(B, N)
-    one.accumulate(ring.reshape(-1), ld, slot, nslots, 4000)
-    one.accumulate(ring.reshape(-1), ld, slot, nslots, 6000)
-    assert two.nseg == one.nseg == 2
+    for k in range(K):
+        one.accumulate(ring.reshape(-1), ld, slot, nslots, 4000 + 2000 * k)
+    assert two.nseg == one.nseg == K
     p2, psd2 = two.peak(want_psd=True)
     p1, _ = one.peak(want_psd=True)
     torch.cuda.synchronize()
