@@ -179,6 +179,14 @@ __device__ __forceinline__ void emit(const BoldArgs& a, const BoldLayout& L, dou
 // COPY: time-major fp32 input, also written out node-major (copy[c*copy_ld + tt])
 // through a 256-column x 32-sample LDS tile flushed as 128-B rows.
 constexpr int kCopyT = 32;
+#ifndef WC_BOLD_PINGPONG
+#define WC_BOLD_PINGPONG 1  // the steady loop's two sample batches in static ping-pong buffers (0: one
+                            // buffer copied per batch; 1.3% slower, profiles/r03_ab_bold_pp.log)
+#endif
+#ifndef WC_BOLD_BATCH
+#define WC_BOLD_BATCH 16    // samples per load batch (divides kCopyT)
+#endif
+constexpr int kBat = WC_BOLD_BATCH;
 #ifndef WC_BOLD_COPY_WPS
 #define WC_BOLD_COPY_WPS 4  // workgroups (of 4 waves) per CU for the steady copy instantiation: 128 VGPRs,
                             // 8 spilled, 6% faster than 3 (tools/ab_multi.sh, profiles/r03_ab_bold.log)
@@ -361,29 +369,29 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? WC_
     // the next batch's loads are also issued BEFORE the previous 32-sample tile's
     // row stores: vmcnt retires in issue order, so a load issued after those stores
     // would wait for them (that ordering cost 7 ms per chunk at C3).
-    auto load = [&](ET (&x)[16], int64_t tb) {
+    auto load = [&](ET (&x)[kBat], int64_t tb) {
         if (sizeof(ET) == 4 && e_ld == 0) {
             // time-major fp32: one descriptor per batch (uniform base E + tb*C, the row
             // offset j*C*4 in an SGPR), the lane's column offset in one VGPR
-            const int64_t nrow = Tc - tb < 16 ? Tc - tb : 16;
+            const int64_t nrow = Tc - tb < kBat ? Tc - tb : kBat;
             const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<ET*>(E) + tb * a.C, 0, (int)(nrow * a.C * 4), 0x00020000);
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
+            for (int j = 0; j < kBat; ++j) {
                 const int jj = j < nrow ? j : 0;
                 const uint32_t u = __builtin_amdgcn_raw_buffer_load_b32(ers, (int)(ce * 4), (int)(jj * a.C * 4), 0);
                 x[j] = (ET)__uint_as_float(u);
             }
         } else {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
+            for (int j = 0; j < kBat; ++j) {
                 const int64_t tt = tb + j < Tc ? tb + j : tb;
                 x[j] = E[e_ld ? ce * e_ld + tt : tt * a.C + ce];
             }
         }
     };
     // STEADY launches cover only 16 <= i <= n - 17 (the host splits the chunk)
-    auto process = [&](const ET (&x)[16], int64_t tb) {
+    auto process = [&](const ET (&x)[kBat], int64_t tb) {
         const int k0 = (int)(tb % kCopyT);
         if constexpr (COPY) {
             if (k0 == 0 && tb > 0) flush(tb - kCopyT, kCopyT);
@@ -393,9 +401,9 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? WC_
         const int64_t ib = t0 + tb - neq;
         const int dec = (int)a.cfg.dec;
         int mb = STEADY ? (int)(ib / dec) : 0, rb = STEADY ? (int)(ib - (int64_t)mb * dec) : 0;
-        const int rem = Tc - tb < 16 ? (int)(Tc - tb) : 16;  // samples of this batch inside the chunk
+        const int rem = Tc - tb < kBat ? (int)(Tc - tb) : kBat;  // samples of this batch inside the chunk
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < kBat; ++j) {
             if constexpr (COPY) tile[lane * (kCopyT + 1) + k0 + j] = (float)x[j];
             if (STEADY) {
                 if (j < rem) steady((double)x[j], rb, mb);
@@ -408,15 +416,30 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? WC_
             }
         }
     };
-    ET xa[16];
+    ET xa[kBat];
     load(xa, 0);
-    for (int64_t tb = 0; tb < Tc; tb += 16) {
+#if WC_BOLD_PINGPONG
+    if constexpr (STEADY) {
+        // two batches per iteration with static buffers: no register copy of in-flight loads (a copy
+        // would wait for them, vmcnt retiring in order)
+        ET xb[kBat];
+        int64_t tb = 0;
+        for (; tb + kBat < Tc; tb += 2 * kBat) {
+            load(xb, tb + kBat);
+            process(xa, tb);
+            if (tb + 2 * kBat < Tc) load(xa, tb + 2 * kBat);
+            process(xb, tb + kBat);
+        }
+        if (tb < Tc) process(xa, tb);
+    } else
+#endif
+    for (int64_t tb = 0; tb < Tc; tb += kBat) {
         if (STEADY) {
-            ET xb[16];
-            if (tb + 16 < Tc) load(xb, tb + 16);
+            ET xb[kBat];
+            if (tb + kBat < Tc) load(xb, tb + kBat);
             process(xa, tb);
 #pragma unroll
-            for (int j = 0; j < 16; ++j) xa[j] = xb[j];
+            for (int j = 0; j < kBat; ++j) xa[j] = xb[j];
         } else {
             if (tb > 0) load(xa, tb);
             process(xa, tb);
