@@ -200,6 +200,7 @@ def main():
     dev = torch.device("cuda", local)
     bt = Batch(sc, G, S, keys, p, precision=args.precision, device=dev)
     R, CH, NSLOT = 20, 1000, 6           # record every 20 steps; 1000-sample chunks; 6-slot ring (Welch pairs)
+    WELCH_SEG = 4000                     # nperseg (whole_sweep_both.py:90), hop WELCH_SEG / 2
     LD = CH * NSLOT
     EULER = CH * R                       # Euler steps per chunk
     CHUNKS = 2                           # chunks per bench step (one Welch segment per step: a launch of two
@@ -216,8 +217,8 @@ def main():
         welch = WelchAccumulator(B, N, dev)
     # (no separate transient launch: every wc_sde_kernel launch of the run is one 20,000-step chunk,
     # so the rocprofv3 average of the kernel equals the per-launch time reported here)
-    state = {"k": 0, "timed": False}
-    ev = {"sde": [], "bold": [], "welch": []}
+    state = {"k": 0, "timed": False, "pending": False}
+    ev = {"sde": [], "bold": [], "welch": [], "welch1": []}
 
     def timed(name, fn):
         if not state["timed"]:
@@ -243,11 +244,23 @@ def main():
                 if bold is not None:
                     timed("bold", lambda: bold.feed(ring, CH, e_ld=LD, offset=slot * CH))
             state["k"] = k = k + 1
-            if welch is not None and k >= NSLOT and k % 4 == 2:
-                timed("welch", lambda: welch.accumulate(ring, LD, CH, NSLOT, (k - NSLOT) * CH, nseg=2))
+        # the segment ending at this step's last sample: held for one step and launched with the next
+        # one (two per launch, as the pipeline does); flush_welch() launches a held one alone
+        if welch is not None and state["k"] * CH >= WELCH_SEG:
+            if state["pending"]:
+                k = state["k"]
+                timed("welch", lambda: welch.accumulate(ring, LD, CH, NSLOT, k * CH - WELCH_SEG - WELCH_SEG // 2, nseg=2))
+            state["pending"] = not state["pending"]
+
+    def flush_welch():
+        if welch is not None and state["pending"]:
+            k = state["k"]
+            timed("welch1", lambda: welch.accumulate(ring, LD, CH, NSLOT, k * CH - WELCH_SEG))
+            state["pending"] = False
 
     for _ in range(args.warmup):
         step()
+    flush_welch()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -256,6 +269,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    flush_welch()  # (an odd step count: the last segment alone, inside the timed region)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -268,6 +282,7 @@ def main():
     kern = {k: (sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None) for k, v in ev.items()}
     if kern["welch"] is not None:
         kern["welch"] /= 2  # ms per segment (each launch takes two)
+    kern.pop("welch1")  # (a lone last segment of an odd step count: timed in the step, not reported)
     B_all = B
     if dist:  # strong scaling: shards may differ by one simulation
         t = torch.tensor([B], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.int64)
