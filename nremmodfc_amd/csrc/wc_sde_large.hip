@@ -720,6 +720,17 @@ struct PArgs {
 __host__ __device__ __forceinline__ uint32_t pimg_unit(const PGeo& g, int c, int sb, int p, int t) {
     return (uint32_t)((((size_t)c * g.SBp + sb) * kParts + p) * kPT + t);
 }
+#ifndef WC_PIMG16
+#define WC_PIMG16 1  // the E image in 16-B units of one node tile (hi | lo), one store per lane and tile
+                     // (0: 8-B halves of two tiles per unit; 4.5% slower, profiles/r03_c5_pimg16.log)
+#endif
+// WC_PIMG16 layout: unit (k-chunk c, simulation block sb, simulation tile t, half h) of 64 lanes x
+// 16 B, lane (g, j) holding [hi | lo] of nodes 16 (2c + h) + 4g + r, r < 4, of simulation 80 sb +
+// 16 t + j: the publishing wave (node tile 2c + h) writes whole 16-B pieces, the chunk of a block
+// is still 10 contiguous KB, and the staging splits each piece into the two parts' B fragments
+__host__ __device__ __forceinline__ uint32_t pimg_unit16(const PGeo& g, int c, int sb, int t, int h) {
+    return (uint32_t)((((size_t)c * g.SBp + sb) * kPT + t) * 2 + h);
+}
 
 // DIAG (timing ablations only, diag build, WCSDE_PERSISTENT=2..5; results are wrong): 1 = no MFMA, 2 = no
 // epilogue arithmetic, 3 = no K-loop operand loads, 4 = no hand-off waits
@@ -787,12 +798,19 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         for (int t = 0; t < kPT; ++t) {
             f16x4 ph[kParts];
             split2h(E[t], ph[0], ph[1]);
+#if WC_PIMG16
+            typedef unsigned u4s __attribute__((ext_vector_type(4)));
+            const u2 h0 = __builtin_bit_cast(u2, ph[0]), h1 = __builtin_bit_cast(u2, ph[1]);
+            const uint32_t unit = buf * img_units + pimg_unit16(g, mt >> 1, sb, t, mt & 1);
+            __builtin_amdgcn_raw_buffer_store_b128(u4s{h0.x, h0.y, h1.x, h1.y}, xrs, (int)((unit * 64 + lane) * 16), 0, 16);
+#else
 #pragma unroll
             for (int p = 0; p < kParts; ++p) {
                 const uint32_t unit = buf * img_units + pimg_unit(g, mt >> 1, sb, p, t);
                 const int off = (int)((unit * 64 + lane) * 16 + (mt & 1) * 8);
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, ph[p]), xrs, off, 0, 16);
             }
+#endif
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -877,12 +895,25 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     // WC_PPAIR: chunks c, c + 1 (a pair) staged together into pair stage (c / 2) & 1 behind ONE
     // barrier; that stage was last read two pairs ago, before the previous pair's barrier.  The
     // pair's A operands are taken before the next pair's loads overwrite fa.
+    // one staged 16-B unit-lane ul (0..639) of a chunk into ldsB stage `st` (stage row h)
+    auto stage_put = [&](int st, int h, int ul, u4 v) {
+#if WC_PIMG16
+        // unit (t, hh) = ul / 64: hi -> part 0's fragment of tile t, lo -> part 1's, half hh of each
+        const int u = ul >> 6, ln = ul & 63, t = u >> 1, hh = u & 1;
+        unsigned* b0 = reinterpret_cast<unsigned*>(&ldsB[st][h][t][ln]) + 2 * hh;
+        unsigned* b1 = reinterpret_cast<unsigned*>(&ldsB[st][h][kPT + t][ln]) + 2 * hh;
+        *reinterpret_cast<u2*>(b0) = u2{v.x, v.y};
+        *reinterpret_cast<u2*>(b1) = u2{v.z, v.w};
+#else
+        reinterpret_cast<u4*>(&ldsB[st][h][0][0])[ul] = v;
+#endif
+    };
     auto do_pair = [&](int c, int buf, f4 (&acc)[kPT]) {
         const int ps = (c >> 1) & 1;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            reinterpret_cast<u4*>(&ldsB[ps][h][0][0])[tid] = rb[h][0];
-            if (tid < 128) reinterpret_cast<u4*>(&ldsB[ps][h][0][0])[512 + tid] = rb[h][1];
+            stage_put(ps, h, tid, rb[h][0]);
+            if (tid < 128) stage_put(ps, h, 512 + tid, rb[h][1]);
         }
         __syncthreads();
         const f16x8 a00 = c < res ? ldsA[c][w][0][lane] : fa[0][0];
@@ -897,8 +928,8 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         mfma_chunk(c + 1, a10, a11, ldsB[ps][1], acc);
     };
     auto do_chunk = [&](int c, int slot, int buf, f4 (&acc)[kPT]) {
-        reinterpret_cast<u4*>(&ldsB[slot][0][0][0])[tid] = rb[slot][0];
-        if (tid < 128) reinterpret_cast<u4*>(&ldsB[slot][0][0][0])[512 + tid] = rb[slot][1];
+        stage_put(slot, 0, tid, rb[slot][0]);
+        if (tid < 128) stage_put(slot, 0, 512 + tid, rb[slot][1]);
         __syncthreads();  // stage `slot` was last read at chunk c - 2, before the previous barrier
         // (each wave reads only its own ldsA slice, written by itself before the step loop)
         const f16x8 a0 = c < res ? ldsA[c][w][0][lane] : fa[slot][0];
