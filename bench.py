@@ -209,8 +209,8 @@ def main():
     ring = torch.empty(C * LD, dtype=bt.rec_dtype, device=dev)
     # fp32 + consumers: the integrator writes each chunk time-major, the BOLD pass transposes it
     # into the node-major Welch ring (the sweep pipeline's layout, nremmodfc_amd/pipeline.py)
-    tmaj = torch.empty(CH * C, dtype=bt.rec_dtype, device=dev) \
-        if (args.precision == "f32" and not args.sde_only) else None
+    # (--sde-only records the same way, time-major, so it times exactly the pipeline's integrator work)
+    tmaj = torch.empty(CH * C, dtype=bt.rec_dtype, device=dev) if args.precision == "f32" else None
     bold = welch = None
     if not args.sde_only:
         bold = BoldStream(C, max(n_total, 300_000), NEQ, 1000, p.dt * p.downsamp, dev)
@@ -238,7 +238,8 @@ def main():
             slot = k % NSLOT
             if tmaj is not None:
                 timed("sde", lambda: bt.integrate(EULER, 2.0, R, tmaj))
-                timed("bold", lambda: bold.feed(tmaj, CH, e_ld=0, copy=ring, copy_ld=LD, copy_offset=slot * CH))
+                if bold is not None:
+                    timed("bold", lambda: bold.feed(tmaj, CH, e_ld=0, copy=ring, copy_ld=LD, copy_offset=slot * CH))
             else:
                 timed("sde", lambda: bt.integrate(EULER, 2.0, R, ring[slot * CH:], rec_ld=LD))
                 if bold is not None:
