@@ -229,7 +229,14 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? WC_
         for (int i = 0; i < 8; ++i) {
             const int q = lane + 64 * i, col = q >> 3, part = q & 7;
             const float* srow = tile + col * (kCopyT + 1) + 4 * part;
+#ifdef WC_BOLD_COPY_BLOCKED
+            // TIMING PROBE ONLY (wrong layout for Welch): the wave's 64 x 32 tile as one contiguous
+            // 8-KB run, to price the row stores' scatter (profiles/r03_bold_blocked_probe.log)
+            const int off = (len == kCopyT) ? (int)((tt0 / kCopyT) * 8192 + q * 16)
+                                            : (int)(((int64_t)col * copy_ld + tt0 + 4 * part) * 4);
+#else
             const int off = (int)(((int64_t)col * copy_ld + tt0 + 4 * part) * 4);
+#endif
             if (vec && len == kCopyT) {
                 typedef unsigned u4 __attribute__((ext_vector_type(4)));
                 const u4 v = {__float_as_uint(srow[0]), __float_as_uint(srow[1]), __float_as_uint(srow[2]),
