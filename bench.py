@@ -12,10 +12,12 @@ chunks of 20,000 Euler steps of the recorded phase (tau_ip = 2, E stored every
 4000-sample Welch segment (a launch of the last two every other step) -- the steady state of
 the sweep pipeline (nremmodfc_amd/pipeline.py); inputs and state resident in
 HBM.  --sde-only times the integrator alone.  With --gpus N (torchrun, one rank per
-GPU) each rank runs its own 20,000-simulation shard (seeds 50r..50r+49):
-weak scaling, no data-path collective.  --scaling strong instead splits the ONE
-20,000-simulation C3 sweep over the ranks with the reference's round robin
-(simulation i on rank i % N, whole_sweep_both.py:63-64).
+GPU) the ONE 20,000-simulation C3 sweep north_star names is split over the ranks
+with the reference's round robin (simulation i on rank i % N,
+whole_sweep_both.py:63-64; strong scaling, the default, no data-path
+collective); the weak-scaling job (every rank its own 20,000-simulation sweep,
+seeds 50r..50r+49) is timed after it and reported as `weak_scaling`
+(--scaling weak makes it the headline instead).
 
 Prints ONE JSON line (rank 0).
 """
@@ -101,12 +103,10 @@ def cpu_baseline_numpy(steps=150_000):
     return {"value": value, "unit": "node-timesteps/sec", "cores": ncores, "kind": "port",
             "cores_available": avail, "cores_cap": CPU_SHARE,
             "per_core": {"mean": float(np.mean(per_core)), "min": float(min(per_core))},
-            "extrapolated_all_available_cores": float(np.mean(per_core)) * avail,
             "sample": f"{ncores} processes x 1 sim x {steps} Euler steps of the C3 cell (0.16, 7.68), N=90: the "
                       f"reference's NumPy loop (oracle/numpy_run.py, bit-identical to netwWilsonCowanPlastic.py's "
                       f"run() under replayed noise), numpy's normal draws, 1 BLAS thread each; {wall:.1f} s wall",
-            "note": "cores capped at one GPU's host share on the box (CPU_SHARE); extrapolated_all_available_cores "
-                    "= mean per-core rate x cores_available, not measured"}
+            "note": "cores capped at one GPU's host share on the box (CPU_SHARE)"}
 
 
 def cpu_baseline_compiled(sc, seconds=8.0, steps=2000):
@@ -129,75 +129,33 @@ def cpu_baseline_compiled(sc, seconds=8.0, steps=2000):
     ns = B * sc.shape[0] * steps * n
     return {"value": ns / total, "unit": "node-timesteps/sec", "cores": ncores, "kind": "port",
             "cores_available": avail, "cores_cap": CPU_SHARE,
-            "extrapolated_all_available_cores": ns / total / ncores * avail,
             "sample": f"{B} sims x {steps * n} Euler steps of the C3 grid (tau_ip=2, E recorded every "
-                      f"20 steps), oracle/wc_oracle.c fp64, OpenMP over simulations, {total:.1f} s"}
+                      f"20 steps), oracle/wc_oracle.c fp64 (the compiled loop numba gives the reference), "
+                      f"OpenMP over simulations, {ncores} threads, {total:.1f} s",
+            "note": "cores capped at one GPU's host share on the box (CPU_SHARE = 16 of the affinity mask's "
+                    "cores_available); profiles/r04_cpu_scaling.log has the per-core rate at 1..16 cores"}
 
 
 def cpu_baseline(sc, seconds=8.0, steps=2000):
-    """The reference-shaped NumPy leg (the reported baseline) with the compiled C port beside it;
-    `seconds` sizes both (about 2 x seconds of CPU work in total)."""
-    out = cpu_baseline_numpy(steps=max(2000, int(seconds * 20_000)))
-    out["compiled_port"] = cpu_baseline_compiled(sc, seconds, steps)
+    """The reported baseline is the compiled port (oracle/wc_oracle.c): the reference decorates run()
+    and wilsonCowan with numba's @njit (netwWilsonCowanPlastic.py:77,86) and cannot be imported
+    without numba, so as shipped its loop always runs compiled.  The interpreted NumPy restatement
+    (the same loop without the JIT) is reported beside it as `numpy_interpreted`; `seconds` sizes
+    both (about 2 x seconds of CPU work in total)."""
+    out = cpu_baseline_compiled(sc, seconds, steps)
+    out["numpy_interpreted"] = cpu_baseline_numpy(steps=max(2000, int(seconds * 20_000)))
+    out["numpy_interpreted"]["kind"] = "interpreted"
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--precision", default="f32", choices=("f32", "f64"))
-    ap.add_argument("--config", default="c3", choices=("c3", "c5"),
-                    help="c3: 20,000 sims x 90 nodes per GPU (the metric's config); c5: the 1000-node "
-                         "synthetic connectome, 2,500 sims per GPU (20,000 over 8 GPUs)")
-    ap.add_argument("--sde-only", action="store_true",
-                    help="time the integrator alone (no streamed BOLD / Welch consumers)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
-                    help="nccl (RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0)
-    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
-                    help="weak: 20,000 (c3) / 2,500 (c5) sims per rank; strong: the one c3 sweep (20,000 sims) or "
-                         "c5 sweep (20,000 sims over 8 GPUs = 2,500 x 8) split round-robin over the ranks")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.dist_backend == "gloo":  # rehearsal: ranks may share a device
-        local %= torch.cuda.device_count()
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
-
+def run_workload(sc, G, S, keys, p, args, dev, dist, steps, warmup):
+    """Time `steps` bench steps of one batch after `warmup` untimed ones; a barrier and a device
+    synchronisation on both sides, the maximum over ranks.  -> (seconds, mean ms per kernel)."""
     from nremmodfc_amd.sigchain import NEQ, BoldStream, WelchAccumulator
 
-    if args.scaling == "strong":  # one sweep, the reference's round robin (whole_sweep_both.py:63-64)
-        G, S, keys = sweep_batch(0)
-        if args.config == "c5":  # the C5 job: 20,000 sims over 8 GPUs; strong scaling of 1/8 of it per GPU at N=8
-            G, S, keys = G[:2500 * 8], S[:2500 * 8], keys[:2500 * 8]
-        mine = np.arange(len(keys)) % world == rank
-        G, S, keys = G[mine], S[mine], keys[mine]
-        sc = datasets.synthetic_sc(1000) if args.config == "c5" else datasets.load_sc()
-    elif args.config == "c5":
-        sc = datasets.synthetic_sc(1000)
-        G, S, keys = sweep_batch(rank)
-        lo = rank * 2500 % len(keys)
-        G, S, keys = G[lo:lo + 2500], S[lo:lo + 2500], keys[lo:lo + 2500]
-    else:
-        sc = datasets.load_sc()
-        G, S, keys = sweep_batch(rank)
     N = sc.shape[0]
     B = len(keys)
     C = B * N
-    p = driver_params()
-    dev = torch.device("cuda", local)
     bt = Batch(sc, G, S, keys, p, precision=args.precision, device=dev)
     R, CH, NSLOT = 20, 1000, 6           # record every 20 steps; 1000-sample chunks; 6-slot ring (Welch pairs)
     WELCH_SEG = 4000                     # nperseg (whole_sweep_both.py:90), hop WELCH_SEG / 2
@@ -205,7 +163,7 @@ def main():
     EULER = CH * R                       # Euler steps per chunk
     CHUNKS = 2                           # chunks per bench step (one Welch segment per step: a launch of two
                                          # overlapping segments every other step, as the sweep pipeline runs them)
-    n_total = (args.warmup + args.steps) * CHUNKS * CH + NEQ
+    n_total = (warmup + steps) * CHUNKS * CH + NEQ
     ring = torch.empty(C * LD, dtype=bt.rec_dtype, device=dev)
     # fp32 + consumers: the integrator writes each chunk time-major, the BOLD pass transposes it
     # into the node-major Welch ring (the sweep pipeline's layout, nremmodfc_amd/pipeline.py)
@@ -259,7 +217,7 @@ def main():
             timed("welch1", lambda: welch.accumulate(ring, LD, CH, NSLOT, k * CH - WELCH_SEG))
             state["pending"] = False
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     flush_welch()
     torch.cuda.synchronize()
@@ -268,7 +226,7 @@ def main():
     torch.cuda.synchronize()
     state["timed"] = True
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     flush_welch()  # (an odd step count: the last segment alone, inside the timed region)
     torch.cuda.synchronize()
@@ -284,6 +242,79 @@ def main():
     if kern["welch"] is not None:
         kern["welch"] /= 2  # ms per segment (each launch takes two)
     kern.pop("welch1")  # (a lone last segment of an odd step count: timed in the step, not reported)
+    return elapsed, kern
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--precision", default="f32", choices=("f32", "f64"))
+    ap.add_argument("--config", default="c3", choices=("c3", "c5"),
+                    help="c3: 20,000 sims x 90 nodes per GPU (the metric's config); c5: the 1000-node "
+                         "synthetic connectome, 2,500 sims per GPU (20,000 over 8 GPUs)")
+    ap.add_argument("--sde-only", action="store_true",
+                    help="time the integrator alone (no streamed BOLD / Welch consumers)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--scaling", default=None, choices=("weak", "strong"),
+                    help="strong (the c3 default): the one c3 sweep (20,000 sims) or c5 sweep (20,000 sims over 8 "
+                         "GPUs = 2,500 x 8) split round-robin over the ranks; weak (the c5 default): 20,000 (c3) / "
+                         "2,500 (c5) sims per rank")
+    ap.add_argument("--weak-steps", type=int, default=2,
+                    help="c3, strong, N > 1: also time this many steps of the weak-scaling job (every rank its "
+                         "own 20,000-sim sweep) and report its aggregate as weak_scaling (0: skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":  # rehearsal: ranks may share a device
+        local %= torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+
+    if args.scaling is None:  # c3: the ONE sweep north_star names, split over the ranks (identical at N = 1)
+        args.scaling = "strong" if args.config == "c3" else "weak"
+    if args.scaling == "strong":  # one sweep, the reference's round robin (whole_sweep_both.py:63-64)
+        G, S, keys = sweep_batch(0)
+        if args.config == "c5":  # the C5 job: 20,000 sims over 8 GPUs; strong scaling of 1/8 of it per GPU at N=8
+            G, S, keys = G[:2500 * 8], S[:2500 * 8], keys[:2500 * 8]
+        mine = np.arange(len(keys)) % world == rank
+        G, S, keys = G[mine], S[mine], keys[mine]
+        sc = datasets.synthetic_sc(1000) if args.config == "c5" else datasets.load_sc()
+    elif args.config == "c5":
+        sc = datasets.synthetic_sc(1000)
+        G, S, keys = sweep_batch(rank)
+        lo = rank * 2500 % len(keys)
+        G, S, keys = G[lo:lo + 2500], S[lo:lo + 2500], keys[lo:lo + 2500]
+    else:
+        sc = datasets.load_sc()
+        G, S, keys = sweep_batch(rank)
+    N = sc.shape[0]
+    B = len(keys)
+    p = driver_params()
+    dev = torch.device("cuda", local)
+    elapsed, kern = run_workload(sc, G, S, keys, p, args, dev, dist, args.steps, args.warmup)
+    weak = None
+    if dist and args.scaling == "strong" and args.config == "c3" and args.weak_steps > 0:
+        # the weak-scaling aggregate beside it: every rank its own 20,000-simulation sweep (seeds 50r..)
+        torch.cuda.empty_cache()
+        Gw, Sw, kw = sweep_batch(rank)
+        ew, kern_w = run_workload(sc, Gw, Sw, kw, p, args, dev, dist, args.weak_steps, 1)
+        nsw = len(kw) * world * N * 20 * 1000 * 2 * args.weak_steps
+        weak = {"value": nsw / ew, "ms_per_step": ew / args.weak_steps * 1e3, "steps": args.weak_steps,
+                "sims_per_gpu": len(kw), "sims_total": len(kw) * world, "kernel_ms": kern_w}
+    EULER, CHUNKS, R = 20 * 1000, 2, 20
     B_all = B
     if dist:  # strong scaling: shards may differ by one simulation
         t = torch.tensor([B], device=dev if args.dist_backend == "nccl" else "cpu", dtype=torch.int64)
@@ -409,6 +440,7 @@ def main():
                    "record_every": R, "parallelism": f"sims sharded x{world} ({args.scaling} scaling)"},
         "roofline": roof,
         "kernel_ms": kern,
+        "weak_scaling": weak,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
         out["cpu_baseline"] = cpu_baseline(sc, seconds=args.cpu_seconds)

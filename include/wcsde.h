@@ -185,8 +185,9 @@ int wc_hma(int B, int N, double* fc, double* hin, double* hse, double* hin_node,
  * LDS) from the eigensystem of F = (max(FC,0) + max(FC,0)^T)/2 computed by the
  * caller on the device: lam [B][N] eigenvalues (any order), vt [B][N][N] with row
  * j the eigenvector of lam[j].  Ranks |lam| (stable, descending), walks the
- * levels (HMA.py:62-101), Balance and nodal_measures as wc_hma.  N <= 6700
- * (LDS label arrays). */
+ * levels (HMA.py:62-101), Balance and nodal_measures as wc_hma.  N <= 4096
+ * (the label arrays take 40 B per node of the 160 KB LDS; larger N returns
+ * WC_EUNSUPPORTED). */
 int wc_hma_modes(int B, int N, const double* lam, const double* vt, double* hin, double* hse,
                  double* hin_node, double* hse_node, int* clus_num, double* sv, void* stream);
 

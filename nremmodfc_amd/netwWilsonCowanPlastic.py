@@ -93,15 +93,16 @@ def _params():
                     rI=rI, mu=mu, sigmaI=sigmaI, D=D, dtSim=dtSim, dt=dt)
 
 
-_rhs_step = 0  # Philox step of the next wilsonCowan() call: each call draws fresh noise (wc:80)
+RHS_STREAM = 0xFFFFFFFF  # Philox stream of wilsonCowan()'s noise: not run()'s (0) nor a sweep cell's
+_rhs_steps = {}  # sid -> Philox step of that sid's next wilsonCowan() call: each call draws fresh noise (wc:80)
 
 
 def _wilsonCowan(t, X, sigmaE, mu, tau_ip, G):
     """wilsonCowan(t, X, sigmaE, mu, tau_ip, G) of wc:77-83 -> (3, N) float64 derivatives
     (dE/dt, dI/dt, da_ie/dt), evaluated on the device (wc_rhs).  Like the reference it draws
-    new noise on every call: the normals of Philox step 0, 1, 2, ... of the `sid` stream
-    (the integrator's normals at those global steps).  `t` is unused, as in the reference."""
-    global _rhs_step
+    new noise on every call: the normals of Philox step 0, 1, 2, ... of key (sid, RHS_STREAM),
+    counted per sid, so they are independent of the normals run() draws for the same sid
+    (stream 0).  `t` is unused, as in the reference."""
     from . import _lib
     X = np.ascontiguousarray(X, dtype=np.float64)
     cm = np.asarray(CM, dtype=np.float64)
@@ -114,13 +115,14 @@ def _wilsonCowan(t, X, sigmaE, mu, tau_ip, G):
     tens = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
     g = tens(np.broadcast_to(np.asarray(G, dtype=np.float64), (n,)))
     s = tens(np.broadcast_to(np.asarray(sigmaE, dtype=np.float64), (n,)))
-    keys = torch.from_numpy(sim_keys([sid], [0]).view(np.int64).copy()).to(dev)
+    keys = torch.from_numpy(sim_keys([sid], [RHS_STREAM]).view(np.int64).copy()).to(dev)
+    step = _rhs_steps.get(int(sid), 0)
     x = tens(X)
     out = torch.empty_like(x)
     rc = _lib.lib().wc_rhs(p.to_c(), 1, n, _lib.ptr(tens(cm)), _lib.ptr(g), _lib.ptr(s), _lib.ptr(keys),
-                           _rhs_step, float(tau_ip), _lib.ptr(x), _lib.ptr(out), _lib.stream_handle())
+                           step, float(tau_ip), _lib.ptr(x), _lib.ptr(out), _lib.stream_handle())
     _lib.check(rc, "wc_rhs")
-    _rhs_step += 1
+    _rhs_steps[int(sid)] = step + 1
     return out.cpu().numpy()
 
 

@@ -152,6 +152,8 @@ def hma(fc, want_clus_num=False):
                       _lib.ptr(out["hse_node"]), _lib.ptr(cn), _lib.ptr(out["sv"]), _lib.stream_handle())
         _lib.check(rc, "wc_hma")
         return _with_cn(out, cn)
+    if N > HMA_MODES_MAX_N:  # fail before the eigensolver, not in wc_hma_modes
+        raise _lib.WCSDEError(f"hma: N = {N} > {HMA_MODES_MAX_N} (wc_hma_modes keeps 40 B of labels per node in LDS)")
     # N > 96: F and V no longer fit one workgroup's LDS.  The eigensystem of the symmetrised
     # positive part comes from the batched device eigensolver (rocSOLVER through torch.linalg.eigh),
     # everything after it -- ranks, module levels, Balance, nodal measures -- from wc_hma_modes.
@@ -172,6 +174,7 @@ def hma(fc, want_clus_num=False):
 
 
 HMA_JACOBI_MAX_N = 96   # wc_hma: F and V (2 N^2 fp64) in one workgroup's LDS
+HMA_MODES_MAX_N = 4096  # wc_hma_modes: 2 N fp64 + 6 N int32 label arrays (40 N B) in 160 KB of LDS
 HMA_EIGH_BATCH = 64     # N > 96: matrices per eigensolver call (bounds the V buffers)
 
 

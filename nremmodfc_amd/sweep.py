@@ -7,8 +7,10 @@ files into the comma-separated `output/*.txt` that heatmaps.py reads.  Here one
 process per GPU (torchrun / the same SLURM variables) takes its shard of the
 same `itertools.product` list, runs it through the streamed GPU pipeline in
 large batches, appends the same TSV lines (resumable: simulations already in
-the rank's file are skipped), and rank 0 gathers every row over RCCL (one
-all-gather of a float64 table) and writes the collapsed CSV itself.
+the rank's file are skipped), and rank 0 gathers every rank's shard over RCCL
+(one all-gather of a float64 table) and writes the collapsed CSV from the
+gathered rows (the rank files stay for resume; SLURM-array tasks, which have no
+process group, assemble the table from the rank files instead).
 
   python -m nremmodfc_amd.sweep homo      [--seeds 50 --seed0 0] [--grid shipped|script]
   python -m nremmodfc_amd.sweep maps      --map-ids 1 1  [--seeds 25 --seed0 25]
@@ -122,6 +124,20 @@ def done_keys(path):
             if len(p) == len(HEADER):
                 keys.add((int(p[1]), p[2], p[3]))
     return keys
+
+
+def read_rank_rows(path):
+    """{(seed, delta_G, delta_sigma): metric dict} of the rows already in a rank file (as written, %.4f)."""
+    out = {}
+    if not os.path.exists(path):
+        return out
+    with open(path) as f:
+        next(f, None)
+        for line in f:
+            p = line.rstrip("\n").split("\t")
+            if len(p) == len(HEADER):
+                out[(int(p[1]), p[2], p[3])] = {c: float(v) for c, v in zip(METRIC_COLS, p[4:])}
+    return out
 
 
 def append_rows(path, rank, sims, results):
@@ -269,11 +285,54 @@ def rank_files_complete(sims, out, tag, world):
 
 def collapse_sweep(sims, out, tag, world):
     """{tag}.txt (the comma-separated table heatmaps.py reads) and {tag}_rows.npy, both
-    built from the rank files (so rows restored by a resumed run are included)."""
+    built from the rank files (so rows restored by a resumed run are included).  The path
+    of SLURM-array runs, which have no process group; torchrun runs use write_gathered."""
     paths = [os.path.join(out, "temp", f"{tag}_rank{r}") for r in range(world)]
     tmp = os.path.join(out, f".{tag}.txt.{os.getpid()}")
     df = collapse(paths, tmp)
     os.replace(tmp, os.path.join(out, f"{tag}.txt"))
+    return _save_rows(sims, out, tag, df)
+
+
+def shard_table(rank, mine, todo, rows, path):
+    """This rank's whole shard as a rows_table: this run's rows for `todo`, the rows a
+    previous (resumed) run left in the rank's own file for the rest, in shard order."""
+    new = {s.index: r for s, r in zip(todo, rows)}
+    old = read_rank_rows(path) if len(new) < len(mine) else {}
+    have, vals = [], []
+    for s in mine:
+        r = new.get(s.index)
+        if r is None:
+            r = old.get((s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}"))
+        if r is not None:
+            have.append(s)
+            vals.append(r)
+    return rows_table(rank, have, vals)
+
+
+def write_gathered(sims, out, tag, table):
+    """{tag}.txt and {tag}_rows.npy from the gathered rows (rank 0 of a torchrun job): the
+    rows go through the same text the rank files hold (format_row, %.4f) and the same
+    pandas read/write as collapse_sweep, rank-major in shard order, so the two paths write
+    the same bytes; no rank file is read."""
+    import io
+    import pandas as pd
+    by_index = {s.index: s for s in sims}
+    order = np.lexsort((table[:, 1], table[:, 0]))
+    text = ["\t".join(HEADER) + "\n"]
+    for i in order:
+        t = table[i]
+        text.append(format_row(int(t[0]), by_index[int(t[1])], dict(zip(METRIC_COLS, t[4:]))))
+    df = pd.read_csv(io.StringIO("".join(text)), sep="\t")
+    tmp = os.path.join(out, f".{tag}.txt.{os.getpid()}")
+    df.to_csv(tmp, index=False)
+    os.replace(tmp, os.path.join(out, f"{tag}.txt"))
+    return _save_rows(sims, out, tag, df)
+
+
+def _save_rows(sims, out, tag, df):
+    """{tag}_rows.npy: the collapsed table as float64 [n][4 + 16] (rank, index, seed, stream,
+    metrics as printed), sorted by the simulation's index in the reference's product list."""
     index = {(s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}"): s for s in sims}
     table = np.full((len(df), 4 + len(METRIC_COLS)), np.nan)
     for i, r in enumerate(df.itertuples(index=False)):
@@ -396,16 +455,17 @@ def main(argv=None):
         print(perf, flush=True)
         with open(os.path.join(args.out, "temp", f"{tag}_rank{rank}_perf.jsonl"), "a") as f:  # one line per run
             f.write(perf + "\n")
-        gathered = None
-        if dist:  # every rank's rows reach rank 0 over RCCL (its rank file is flushed by then)
-            gathered = gather_table(rows_table(rank, todo, rows), dist, torch.device(device))
-        if launcher == "slurm":
+        if dist:  # the data path: every rank's whole shard reaches rank 0 in one all-gather over RCCL
+            gathered = gather_table(shard_table(rank, mine, todo, rows, path), dist, torch.device(device))
+            if rank == 0:
+                if len(gathered) != len(sims):
+                    raise RuntimeError(f"gathered {len(gathered)} rows for {len(sims)} simulations")
+                write_gathered(sims, args.out, tag, gathered)
+        elif launcher == "slurm":
             if rank_files_complete(sims, args.out, tag, world):  # the last task to finish assembles
                 collapse_sweep(sims, args.out, tag, world)
         elif rank == 0:
-            table = collapse_sweep(sims, args.out, tag, world)
-            if gathered is not None and not set(gathered[:, 1].astype(int)) <= set(table[:, 1].astype(int)):
-                raise RuntimeError("collapsed table is missing rows the ranks gathered")
+            collapse_sweep(sims, args.out, tag, world)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -1,7 +1,8 @@
 """bench.py keeps the driver's JSON contract (task spec).
 
-CPU: the cpu_baseline legs (the reference's NumPy loop, oracle/numpy_run.py, one process per
-core; the compiled C port beside it) on a short sample.
+CPU: the cpu_baseline legs (the compiled C port, the cost of the reference's numba-compiled loop,
+as the value; the interpreted NumPy loop, oracle/numpy_run.py, one process per core, beside it)
+on a short sample.
 GPU: one short bench run as a child process; its single JSON line carries every
 contract key, the roofline and issued-MFMA objects, and consistent arithmetic.
 """
@@ -21,10 +22,11 @@ def test_cpu_baseline_leg():
     from nremmodfc_amd import datasets
     cb = bench.cpu_baseline(datasets.load_sc(), seconds=0.3, steps=200)
     assert cb["kind"] == "port" and cb["unit"] == "node-timesteps/sec"
-    assert cb["value"] > 0 and 1 <= cb["cores"] <= 16 and "oracle/numpy_run.py" in cb["sample"]
+    assert cb["value"] > 0 and 1 <= cb["cores"] <= 16 and "oracle/wc_oracle.c" in cb["sample"]
     assert cb["cores"] == min(cb["cores_available"], cb["cores_cap"])
-    cp = cb["compiled_port"]
-    assert cp["value"] > 0 and "oracle/wc_oracle.c" in cp["sample"] and cp["cores"] == cb["cores"]
+    npy = cb["numpy_interpreted"]
+    assert npy["kind"] == "interpreted" and npy["value"] > 0 and "oracle/numpy_run.py" in npy["sample"]
+    assert npy["cores"] == cb["cores"]
 
 
 @pytest.mark.gpu
@@ -40,7 +42,7 @@ def test_bench_json_contract(cuda):
         assert k in d, k
     assert d["metric"].startswith("node-timesteps/sec") and d["unit"] == "node-timesteps/sec"
     assert d["n_gpus"] == 1 and d["steps"] == 1 and d["warmup"] == 1 and d["higher_is_better"] is True
-    assert d["scaling"] == "weak" and d["vs_baseline"] is None and d["dtype"].startswith("f32")
+    assert d["scaling"] == "strong" and d["vs_baseline"] is None and d["weak_scaling"] is None and d["dtype"].startswith("f32")
     assert "workload" in d["config"] and d["config"]["sims_per_gpu"] == 20000
     # value = node-steps of the timed steps / wall time
     ns = d["config"]["sims_per_gpu"] * d["config"]["nodes"] * d["config"]["euler_steps_per_step"] * d["steps"]

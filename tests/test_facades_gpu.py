@@ -83,17 +83,18 @@ def test_wc_run_checks_globals(cuda):
 
 def test_wilsonCowan_single_evaluation(cuda, sc90):
     """wc.wilsonCowan(t, X, sigmaE, mu, tau_ip, G) (wc:77-83) on the device: the reference's
-    expression in numpy with the same normals (Philox step k of the sid stream on the k-th call)."""
+    expression in numpy with the same normals (Philox step k of key (sid, RHS_STREAM) on the k-th
+    call for that sid; independent of run()'s stream 0 and counted per sid)."""
     from nremmodfc_amd import netwWilsonCowanPlastic as wc
     from nremmodfc_amd.model import sim_keys
     old = {k: getattr(wc, k) for k in ("CM", "P", "rhoE", "sid")}
     try:
         wc.CM, wc.P, wc.rhoE, wc.sid = sc90, 0.4, 0.18, 21
-        wc._rhs_step = 0
+        wc._rhs_steps.clear()
         rng = np.random.default_rng(3)
         X = np.stack([rng.uniform(0.05, 0.4, 90), rng.uniform(0.05, 0.4, 90), rng.uniform(2.3, 2.7, 90)])
         ach = datasets.load_map("DIST_VAChT_feobv_hc18_aghourian")
-        key = int(sim_keys([21], [0])[0])
+        key = int(sim_keys([21], [wc.RHS_STREAM])[0])
         S = lambda x, s, m: 1 / (1 + np.exp(-(x - m) * s))  # noqa: E731
         for k, (G, sig, mu, tau) in enumerate([(0.16, 7.68, 1, 2), (0.16 + 0.1 * ach, 7.5, 1.1, 0.05)]):
             got = wc.wilsonCowan(0.0, X, sig, mu, tau, G)
@@ -105,7 +106,7 @@ def test_wilsonCowan_single_evaluation(cuda, sc90):
                               (I * (E - wc.rhoE)) / tau))
             assert got.shape == (3, 90)
             np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
-        assert wc._rhs_step == 2
+        assert wc._rhs_steps == {21: 2}
     finally:
         for k, v in old.items():
             setattr(wc, k, v)

@@ -15,6 +15,9 @@ for bit -- not by fp64, not by any fp32 path.  What holds, and is asserted here 
     between-seed floor);
   * the seed-averaged FC matches the reference's at its own split-half sampling floor;
   * every metric column's mean over seeds matches the reference's.
+This test therefore has NO pathwise power: any implementation with the right noise mapping lands at
+the ~0.866 same-noise floor (a coupling off by 2^-11 would pass it).  The pathwise gates are the
+short-horizon ones (test_sde_gpu.py: the reference-run replay and test_f32_gate_detects_coupling_error).
 """
 import os
 

@@ -132,6 +132,61 @@ def test_gather_gloo_world2():
         np.testing.assert_allclose(t[:, 4], np.arange(11))
 
 
+def _gathered_path_worker(rank, world, port, out, q):
+    """A torchrun job's end of run: rank 1 resumes (a previous run left part of its shard in its
+    rank file), every rank gathers its whole shard, rank 0 writes the table from the gathered rows."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sims = sweep.homogeneous(1)[:13]
+    mine = sweep.shard(sims, rank, world)
+    rng = np.random.default_rng(rank)
+    rows = [{c: (float(rng.normal()) if j % 5 else float("nan")) for j, c in enumerate(sweep.METRIC_COLS)}
+            for _ in mine]
+    path = os.path.join(out, "temp", f"g_rank{rank}")
+    done = 3 if rank == 1 else 0  # rows of an earlier run of this rank
+    if done:
+        sweep.append_rows(path, rank, mine[:done], rows[:done])
+    have = sweep.done_keys(path)
+    todo = [s for s in mine if (s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") not in have]
+    sweep.append_rows(path, rank, todo, rows[done:])
+    table = sweep.gather_table(sweep.shard_table(rank, mine, todo, rows[done:], path), dist, torch.device("cpu"))
+    if rank == 0:
+        os.makedirs(os.path.join(out, "g"), exist_ok=True)
+        sweep.write_gathered(sims, os.path.join(out, "g"), "g", table)
+    q.put(rank)
+    dist.destroy_process_group()
+
+
+def test_gathered_path_equals_file_path_gloo_world2(tmp_path):
+    """With a process group the collapsed CSV and rows.npy come from the all-gathered rows, not
+    from other ranks' files; they equal the rank-file path's output byte for byte (resumed rows
+    and NaN columns included)."""
+    import socket
+    import torch.multiprocessing as mp
+    out = str(tmp_path)
+    os.makedirs(os.path.join(out, "temp"))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gathered_path_worker, args=(r, 2, port, out, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    assert sorted(q.get(timeout=120) for _ in ps) == [0, 1]
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    sims = sweep.homogeneous(1)[:13]
+    sweep.collapse_sweep(sims, out, "g", 2)  # the file path over the same rank files
+    with open(os.path.join(out, "g", "g.txt"), "rb") as a, open(os.path.join(out, "g.txt"), "rb") as b:
+        ga, fb = a.read(), b.read()
+    assert ga == fb and ga.count(b"\n") == 14
+    np.testing.assert_array_equal(np.load(os.path.join(out, "g", "g_rows.npy")), np.load(os.path.join(out, "g_rows.npy")))
+
+
 @pytest.mark.gpu
 def test_sweep_main_short(tmp_path, cuda):
     """End to end: a short-schedule homogeneous sweep of 6 simulations writes

@@ -26,5 +26,10 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o sde -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1; rc=$?
       echo "prof rc=$rc"; tail -3 $OUT/prof.log; find $OUT/prof -name "*stats*" | head
       if [ $rc -ne 0 ]; then echo "STOP after prof"; exit $rc; fi ;;
+    bench64)
+      # the reference-precision line (fp64 throughout) with its kernel trace
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof64 -o f64 -- python3 bench.py --precision f64 --steps ${STEPS64:-2} --warmup 1 --no-cpu-baseline > $OUT/bench64.log 2>&1; rc=$?
+      echo "bench64 rc=$rc"; tail -3 $OUT/bench64.log
+      if [ $rc -ne 0 ]; then echo "STOP after bench64"; exit $rc; fi ;;
   esac
 done
