@@ -4,7 +4,7 @@
 # build, then run the GPU tests of the touched stage.
 #
 #   bash tools/ab.sh <stage> <base .so> [pytest file]
-#     stage: sde (tools/cmp_libs.py), bold (tools/cmp_bold.py), welch (tools/cmp_welch.py)
+#     stage: sde (tools/cmp_libs.py), bold (tools/cmp_bold.py), welch (tools/cmp_welch.py), c5 (tools/cmp_c5.py)
 #
 # The base build is made beforehand on the CPU: stash the change, `python -m nremmodfc_amd._build`,
 # copy nremmodfc_amd/libwcsde.so to tools/dbg/libwcsde_base.so, unstash, rebuild.
@@ -12,7 +12,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp PYTHONPATH=.
 STAGE=$1 BASE=$2 TESTS=${3:-}
-case $STAGE in sde) CMP=tools/cmp_libs.py ;; bold) CMP=tools/cmp_bold.py ;; welch) CMP=tools/cmp_welch.py ;;
+case $STAGE in sde) CMP=tools/cmp_libs.py ;; bold) CMP=tools/cmp_bold.py ;; welch) CMP=tools/cmp_welch.py ;; c5) CMP=tools/cmp_c5.py ;;
   *) echo "unknown stage $STAGE"; exit 2 ;; esac
 OUT=gpurun_out/ab_$STAGE
 mkdir -p $OUT

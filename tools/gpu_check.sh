@@ -1,5 +1,8 @@
 #!/bin/bash
-# One GPU session: parity tests, smoke, short bench, rocprof kernel trace.
+# One GPU session: parity tests, smoke, short bench, rocprof kernel trace; optionally the
+# reference-precision bench (bench64), the full homogeneous sweep with its statistics against the
+# shipped table (sweep) and the CPU baseline against core count (cpu).
+#   STEPS="tests smoke bench prof bench64 sweep cpu" bash tools/gpu_check.sh
 # Stops at the first crash/timeout (exit codes other than 0/1 from pytest).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -31,5 +34,16 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof64 -o f64 -- python3 bench.py --precision f64 --steps ${STEPS64:-2} --warmup 1 --no-cpu-baseline > $OUT/bench64.log 2>&1; rc=$?
       echo "bench64 rc=$rc"; tail -3 $OUT/bench64.log
       if [ $rc -ne 0 ]; then echo "STOP after bench64"; exit $rc; fi ;;
+    sweep)
+      timeout -k 10 600 python -m nremmodfc_amd.sweep homo --out $OUT/homo > $OUT/homo.log 2>&1; rc=$?
+      echo "sweep rc=$rc"; tail -1 $OUT/homo.log | cut -c1-300
+      if [ $rc -ne 0 ]; then echo "STOP after sweep"; exit $rc; fi
+      f=$(ls $OUT/homo/*.txt | head -1)
+      timeout -k 10 300 python tools/validate_stats.py "$f" homo $OUT/homo_stats.json > $OUT/homo_val.log 2>&1 || { echo "validate failed"; tail -5 $OUT/homo_val.log; exit 1; }
+      tail -16 $OUT/homo_val.log ;;
+    cpu)
+      timeout -k 10 300 python -u tools/cpu_scaling.py > $OUT/cpu_scaling.log 2>&1; rc=$?
+      echo "cpu rc=$rc"; cat $OUT/cpu_scaling.log
+      if [ $rc -ne 0 ]; then echo "STOP after cpu"; exit $rc; fi ;;
   esac
 done

@@ -2,7 +2,7 @@
 # ONE rocprofv3 --pmc pass over tools/c5_pmc_run.py (the C5 persistent integrator, one 400-step
 # dispatch), per gpurun call: rocprofv3 writes its CSV and then segfaults in process teardown after
 # the cooperative launch (exit 139 after "tool finalization"), and a call stops at a segfault.
-#   PASS = fetch | write | sqa | sqb  -> gpurun_out/prof_c5/<pass>/ ; then tools/profile_c5_summary.py
+#   PASS = fetch | write | sqa | sqb | tcc (L2 hits and misses)  -> gpurun_out/prof_c5/<pass>/ ; then tools/profile_c5_summary.py
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 P=$1
@@ -12,6 +12,7 @@ case $P in
   fetch) C="FETCH_SIZE" ;;
   write) C="WRITE_SIZE" ;;
   sqa) C="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE" ;;
+  tcc) C="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" ;;
   sqb) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU GRBM_GUI_ACTIVE" ;;
   *) echo "unknown pass $P"; exit 2 ;;
 esac

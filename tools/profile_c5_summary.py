@@ -48,6 +48,28 @@ def sq():
     print(json.dumps(d))
 
 
+def tcc():
+    """L2 (TCC) hit rate of the operand stream: where the connectome rows and the E image come from."""
+    import json, sys
+    sys.path.insert(0, "tools")
+    from pmc_summary import summary
+    (k, t), = summary("gpurun_out/prof_c5/tcc", "persist_kernel").items()
+    STEPS = 400
+    req = t["TCC_HIT_sum"] + t["TCC_MISS_sum"]
+    d = {"kernel": k, "steps": STEPS,
+         "tcc_requests_per_step": req / STEPS, "tcc_hits_per_step": t["TCC_HIT_sum"] / STEPS,
+         "tcc_misses_per_step": t["TCC_MISS_sum"] / STEPS, "l2_hit_rate": t["TCC_HIT_sum"] / req,
+         "ea_read_requests_per_step": t["TCC_EA0_RDREQ_sum"] / STEPS,
+         "unique_operand_bytes_per_step": 8 * (4 * 128 * 25 * 32 * 4 + 8 * 80 * 1024 * 4),
+         "note": "rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum over tools/c5_pmc_run.py 400 (one persist_kernel "
+                 "dispatch, 400 steps; tools/profile_c5_pass.sh tcc). unique_operand_bytes_per_step: per XCD the streamed "
+                 "connectome rows of its 4 node blocks (25 of 32 K chunks; 7 stay in LDS) plus the E image of its 8 "
+                 "simulation blocks, summed over the 8 XCDs (4.2 MB per XCD against a 4 MB L2)."}
+    json.dump(d, open("profiles/pmc_c5_tcc.json", "w"), indent=1)
+    print(json.dumps(d))
+
+
 if __name__ == "__main__":
-    hbm()
-    sq()
+    import sys as _s
+    for f in (_s.argv[1:] or ["hbm", "sq", "tcc"]):
+        {"hbm": hbm, "sq": sq, "tcc": tcc}[f]()
