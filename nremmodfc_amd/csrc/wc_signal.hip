@@ -229,19 +229,7 @@ __global__ void __launch_bounds__(256, (STEADY && sizeof(ET) == 4) ? (COPY ? WC_
         for (int i = 0; i < 8; ++i) {
             const int q = lane + 64 * i, col = q >> 3, part = q & 7;
             const float* srow = tile + col * (kCopyT + 1) + 4 * part;
-#ifdef WC_BOLD_COPY_BLOCKED  // =32: 64 x 32 tiles (8-KB runs); =8: 8-sample blocks (2-KB runs)
-            // TIMING PROBE ONLY (wrong layout for Welch): the wave's 64 x 32 tile as one contiguous
-            // 8-KB run, to price the row stores' scatter (profiles/r03_bold_blocked_probe.log)
-#if WC_BOLD_COPY_BLOCKED == 8  // 8-sample blocks: [.. / 8][64 columns][8 samples], 2-KB runs
-            const int off = (len == kCopyT) ? (int)((((tt0 / 8 + (part >> 1)) * 64 + col) * 8 + (part & 1) * 4) * 4)
-                                            : (int)(((int64_t)col * copy_ld + tt0 + 4 * part) * 4);
-#else
-            const int off = (len == kCopyT) ? (int)((tt0 / kCopyT) * 8192 + q * 16)
-                                            : (int)(((int64_t)col * copy_ld + tt0 + 4 * part) * 4);
-#endif
-#else
             const int off = (int)(((int64_t)col * copy_ld + tt0 + 4 * part) * 4);
-#endif
             if (vec && len == kCopyT) {
                 typedef unsigned u4 __attribute__((ext_vector_type(4)));
                 const u4 v = {__float_as_uint(srow[0]), __float_as_uint(srow[1]), __float_as_uint(srow[2]),
