@@ -526,19 +526,47 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                             }
                     }
                 } else if (live) {
+                    // (N and the record stride laundered here: addresses computed from them cannot be
+                    // hoisted out of the step loop, where they would pin 64-bit VGPR pairs)
+                    int Nn = N;
+                    int64_t ld = a.rec_ld;
+                    asm volatile("" : "+s"(Nn), "+s"(ld));
+                    if (ld == 0 && BN < ((size_t)1 << 29)) {
+                        // time-major (the pipeline's fp32 form): the record row's base is uniform (an SGPR
+                        // pair) and a lane's cells sit at 32-bit element offsets cb + 16 TL(u) + r from it,
+                        // so the stores take the saddr form with immediate offsets and no 64-bit cell
+                        // address is held across the step loop (eight of them had spilled to scratch)
+                        Real* rE = static_cast<Real*>(a.recE) + (size_t)rec_row * BN;
+                        Real* rI = a.recI ? static_cast<Real*>(a.recI) + (size_t)rec_row * BN : nullptr;
+                        Real* rA = a.recA ? static_cast<Real*>(a.recA) + (size_t)rec_row * BN : nullptr;
+                        const uint32_t cb = (uint32_t)bb * (uint32_t)Nn + (uint32_t)(4 * g + R0);
 #pragma unroll
-                    for (int u = 0; u < OT; ++u)
+                        for (int u = 0; u < OT; ++u)
 #pragma unroll
-                        for (int r = 0; r < RW; ++r) {
-                            const int n = 16 * TL(u) + 4 * g + R0 + r;
-                            if (n < N) {
-                                const size_t cc = (size_t)bb * N + n;
-                                const size_t o = a.rec_ld ? cc * a.rec_ld + rec_row : (size_t)rec_row * BN + cc;
-                                static_cast<Real*>(a.recE)[o] = E[u][r] * (Real)kEinv;
-                                if (a.recI) static_cast<Real*>(a.recI)[o] = I[u][r];
-                                if (a.recA) static_cast<Real*>(a.recA)[o] = (Real)A[u][r].get();
+                            for (int r = 0; r < RW; ++r) {
+                                const int n = 16 * TL(u) + 4 * g + R0 + r;
+                                if (n < N) {
+                                    const uint32_t cc = cb + (uint32_t)(16 * TL(u) + r);
+                                    rE[cc] = E[u][r] * (Real)kEinv;
+                                    if (rI) rI[cc] = I[u][r];
+                                    if (rA) rA[cc] = (Real)A[u][r].get();
+                                }
                             }
-                        }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < OT; ++u)
+#pragma unroll
+                            for (int r = 0; r < RW; ++r) {
+                                const int n = 16 * TL(u) + 4 * g + R0 + r;
+                                if (n < N) {
+                                    const size_t cc = (size_t)bb * Nn + n;
+                                    const size_t o = ld ? cc * ld + rec_row : (size_t)rec_row * BN + cc;
+                                    static_cast<Real*>(a.recE)[o] = E[u][r] * (Real)kEinv;
+                                    if (a.recI) static_cast<Real*>(a.recI)[o] = I[u][r];
+                                    if (a.recA) static_cast<Real*>(a.recA)[o] = (Real)A[u][r].get();
+                                }
+                            }
+                    }
                 }
                 ++rec_row;
                 rec_cnt = rec_every;

@@ -29,7 +29,7 @@ def save(out):
             for rep in range(3):
                 torch.cuda.synchronize()
                 t = time.perf_counter()
-                bt.integrate(20000, 2.0, 20, big, rec_ld=1000)
+                bt.integrate(20000, 2.0, 20, big)  # time-major, as the fp32 pipeline and bench.py record
                 torch.cuda.synchronize()
                 dt = time.perf_counter() - t
                 print(f"  20000-step chunk: {dt * 1e3:.2f} ms, {dt / 20000 * 1e6:.3f} us/step", flush=True)
