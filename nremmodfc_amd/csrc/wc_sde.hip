@@ -443,18 +443,26 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     if constexpr (!kFragRegs) __syncthreads();  // A-operand image staged
     publish(0);
 
-    const Real a_ee = (Real)a.a_ee, a_ei = (Real)a.a_ei, a_ii = (Real)a.a_ii;
-    const Real P = (Real)a.P, rhoE = (Real)a.rhoE, rE = (Real)a.rE, rI = (Real)a.rI;
-    const Real mu = (Real)a.mu, slI = Tr<Real>::slope(a.sigmaI), sqdtD = (Real)a.sqdtD;
+    Real a_ee = (Real)a.a_ee, a_ei = (Real)a.a_ei, a_ii = (Real)a.a_ii;
+    Real P = (Real)a.P, rhoE = (Real)a.rhoE, rE = (Real)a.rE, rI = (Real)a.rI;
+    Real mu = (Real)a.mu, slI = Tr<Real>::slope(a.sigmaI), sqdtD = (Real)a.sqdtD;
     // fp32 product path: folded constants (see the kFast update)
     const float Pm = (float)(a.P - a.mu), knoise = (float)(a.sqdtD * (double)kSqrt2Ln2);
     const float cIe = (float)(-a.a_ei * a.sigmaI * 1.4426950408889634);
     const float cIi = (float)(a.a_ii * a.sigmaI * 1.4426950408889634);
     const float cI0 = (float)(a.mu * a.sigmaI * 1.4426950408889634);
     const Real dtE = (Real)(a.dtSim / a.tauE), dtI = (Real)(a.dtSim / a.tauI);
-    const Real dt = (Real)a.dtSim;
+    Real dt = (Real)a.dtSim;
     const Real dtA = (Real)(a.dtSim / a.tau_ip);
-    const Real tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;  // fp64 exact forms
+    Real tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;  // fp64 exact forms
+    if constexpr (sizeof(Real) == 8) {
+        // fp64: the model constants pinned in VGPR pairs.  As wave-uniform doubles they sit in
+        // SGPRs beside the Philox round keys and the ocml polynomial constants, overflow the SGPR
+        // file and come back through v_readlane (262 per step loop, plus their s_nop hazards).
+        asm volatile("" : "+v"(a_ee), "+v"(a_ei), "+v"(a_ii), "+v"(P), "+v"(rhoE), "+v"(rE));
+        asm volatile("" : "+v"(rI), "+v"(mu), "+v"(slI), "+v"(sqdtD), "+v"(dt));
+        asm volatile("" : "+v"(tauE), "+v"(tauI), "+v"(tau_ip));
+    }
     PkConsts pk{};
     if constexpr (kFast && kPk) {
         auto bc = [](float v) { return f2v{v, v}; };
