@@ -114,15 +114,106 @@ __device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t
     for (int i = 0; i < 4; ++i) z[i] *= kSqrt2Ln2;
 }
 
-// fp64: correctly rounded-ish libm (ocml); sincospi reduces 2u exactly
+// ---------------- fp64 elementary functions for the parity path ----------------
+// Straight-line forms for the inputs this build produces (no special cases, no tables), each
+// within 2 ulp of the correctly rounded value (checked against numpy over the input domains);
+// ocml's general exp / log / sincospi and the IEEE division sequence took about half of the fp64
+// integrator's VALU.  Coefficients: Taylor series, their truncation below 5e-18 relative.
+namespace f64m {
+// 2^t, |t| <= 1000: t = n + r, |r| <= 1/2, e^(r ln 2) to degree 13, scaled by 2^n
+__device__ __forceinline__ double exp2(double t) {
+    t = __builtin_fmin(__builtin_fmax(t, -1000.0), 1000.0);
+    const double n = __builtin_rint(t);
+    const double r = t - n;  // exact
+    double p = 1.3691488853904128e-12;
+    p = __builtin_fma(p, r, 2.5678435993488206e-11);
+    p = __builtin_fma(p, r, 4.4455382718708116e-10);
+    p = __builtin_fma(p, r, 7.054911620801123e-09);
+    p = __builtin_fma(p, r, 1.01780860092397e-07);
+    p = __builtin_fma(p, r, 1.321548679014431e-06);
+    p = __builtin_fma(p, r, 1.5252733804059841e-05);
+    p = __builtin_fma(p, r, 0.0001540353039338161);
+    p = __builtin_fma(p, r, 0.0013333558146428443);
+    p = __builtin_fma(p, r, 0.009618129107628477);
+    p = __builtin_fma(p, r, 0.05550410866482158);
+    p = __builtin_fma(p, r, 0.24022650695910072);
+    p = __builtin_fma(p, r, 0.6931471805599453);
+    p = __builtin_fma(p, r, 1.0);
+    return __builtin_ldexp(p, (int)n);
+}
+// 1 / d for a normal positive d: the hardware seed and two Newton steps
+__device__ __forceinline__ double rcp(double d) {
+    double x = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, x, 1.0);
+    x = __builtin_fma(x, e, x);
+    e = __builtin_fma(-d, x, 1.0);
+    return __builtin_fma(x, e, x);
+}
+// ln(v 2^-24) for an odd v < 2^24 (the uniforms u01d): v = f 2^k with f in [1/sqrt2, sqrt2),
+// ln f = 2 atanh(s), s = (f - 1) / (f + 1), |s| <= 0.172, odd series to s^21
+__device__ __forceinline__ double log_u24(uint32_t v) {
+    const int k = 31 - __builtin_clz(v);
+    double f = __builtin_ldexp((double)v, -k);  // [1, 2), exact
+    const bool hi = f > 1.4142135623730951;
+    f = hi ? 0.5 * f : f;
+    const double e = (double)(k - 24 + (hi ? 1 : 0));
+    const double s = (f - 1.0) * rcp(f + 1.0);  // f - 1, f + 1 exact
+    const double s2 = s * s;
+    double p = 0.09523809523809523;
+    p = __builtin_fma(p, s2, 0.10526315789473684);
+    p = __builtin_fma(p, s2, 0.11764705882352941);
+    p = __builtin_fma(p, s2, 0.13333333333333333);
+    p = __builtin_fma(p, s2, 0.15384615384615385);
+    p = __builtin_fma(p, s2, 0.18181818181818182);
+    p = __builtin_fma(p, s2, 0.2222222222222222);
+    p = __builtin_fma(p, s2, 0.2857142857142857);
+    p = __builtin_fma(p, s2, 0.4);
+    p = __builtin_fma(p, s2, 0.6666666666666666);
+    p = __builtin_fma(p, s2, 2.0);
+    return __builtin_fma(e, 0.6931471805599453, __builtin_fma(e, 2.3190468138462996e-17, p * s));
+}
+// (sin, cos)(pi x) for x = v 2^-23 (v odd, < 2^24: x = 2 u01d): x = n/2 + r, |r| <= 1/4 exactly,
+// sin(pi r) and cos(pi r) to r^17 and r^18, rotated by n quarter turns
+__device__ __forceinline__ void sincospi_v23(uint32_t v, double& sn, double& cs) {
+    const uint32_t n = (v + (1u << 21)) >> 22;
+    const double r = __builtin_ldexp((double)((int)v - (int)(n << 22)), -23);
+    const double r2 = r * r;
+    double ps = 7.952054001475513e-07;
+    ps = __builtin_fma(ps, r2, -2.1915353447830217e-05);
+    ps = __builtin_fma(ps, r2, 0.00046630280576761255);
+    ps = __builtin_fma(ps, r2, -0.0073704309457143504);
+    ps = __builtin_fma(ps, r2, 0.08214588661112823);
+    ps = __builtin_fma(ps, r2, -0.5992645293207921);
+    ps = __builtin_fma(ps, r2, 2.5501640398773455);
+    ps = __builtin_fma(ps, r2, -5.16771278004997);
+    ps = __builtin_fma(ps, r2, 3.141592653589793);
+    ps *= r;
+    double pc = -1.3878952462213771e-07;
+    pc = __builtin_fma(pc, r2, 4.303069587032947e-06);
+    pc = __builtin_fma(pc, r2, -0.0001046381049248457);
+    pc = __builtin_fma(pc, r2, 0.0019295743094039231);
+    pc = __builtin_fma(pc, r2, -0.02580689139001406);
+    pc = __builtin_fma(pc, r2, 0.2353306303588932);
+    pc = __builtin_fma(pc, r2, -1.3352627688545895);
+    pc = __builtin_fma(pc, r2, 4.0587121264167685);
+    pc = __builtin_fma(pc, r2, -4.934802200544679);
+    pc = __builtin_fma(pc, r2, 1.0);
+    const uint32_t m = n & 3u;
+    const double a = (m & 1u) ? pc : ps, b = (m & 1u) ? ps : pc;  // quarter turns: swap
+    sn = (m == 2u || m == 3u) ? -a : a;
+    cs = (m == 1u || m == 2u) ? -b : b;
+}
+}  // namespace f64m
+
+// fp64 Box-Muller: sqrt(-2 ln u0) (cos, sin)(2 pi u1) with the straight-line forms above
 __device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, double z[4]) {
     uint32_t x[4];
     philox_ctr(step, q, key, x);
-    const double r0 = sqrt(-2.0 * log(u01d(x[0])));
-    const double r1 = sqrt(-2.0 * log(u01d(x[2])));
+    const double r0 = sqrt(-2.0 * f64m::log_u24(2u * (x[0] >> 9) + 1u));
+    const double r1 = sqrt(-2.0 * f64m::log_u24(2u * (x[2] >> 9) + 1u));
     double s0, c0, s1, c1;
-    sincospi(2.0 * u01d(x[1]), &s0, &c0);
-    sincospi(2.0 * u01d(x[3]), &s1, &c1);
+    f64m::sincospi_v23(2u * (x[1] >> 9) + 1u, s0, c0);
+    f64m::sincospi_v23(2u * (x[3] >> 9) + 1u, s1, c1);
     z[0] = r0 * c0;
     z[1] = r0 * s0;
     z[2] = r1 * c1;
@@ -149,8 +240,9 @@ template <> struct Tr<double> {
     __device__ static __forceinline__ acc_t mfma(double a, double b, acc_t c) {
         return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
     }
+    // 1 / (1 + e^(-(x - mu) s)) as 1 / (1 + 2^t), t = (mu - x) s log2(e) (f64m: about 2 ulp)
     __device__ static __forceinline__ double sig(double x, double mu, double s) {
-        return 1.0 / (1.0 + exp(-(x - mu) * s));
+        return f64m::rcp(1.0 + f64m::exp2((mu - x) * s * 1.4426950408889634));
     }
     __device__ static __forceinline__ double slope(double s) { return s; }
     // f64 16x16x4 C/D row is (lane>>4) + 4*reg; permute so that lane group g,

@@ -455,7 +455,9 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     Real dt = (Real)a.dtSim;
     const Real dtA = (Real)(a.dtSim / a.tau_ip);
     Real tauE = (Real)a.tauE, tauI = (Real)a.tauI, tau_ip = (Real)a.tau_ip;  // fp64 exact forms
+    Real itauE = (Real)(1.0 / a.tauE), itauI = (Real)(1.0 / a.tauI), itau_ip = (Real)(1.0 / a.tau_ip);
     if constexpr (sizeof(Real) == 8) {
+        asm volatile("" : "+v"(itauE), "+v"(itauI), "+v"(itau_ip));
         // fp64: the model constants pinned in VGPR pairs.  As wave-uniform doubles they sit in
         // SGPRs beside the Philox round keys and the ocml polynomial constants, overflow the SGPR
         // file and come back through v_readlane (262 per step loop, plus their s_nop hazards).
@@ -786,9 +788,15 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 const Real xI = a_ei * e - a_ii * in;
                 const Real SI = Tr<Real>::sig(xI, mu, slI);
                 if constexpr (sizeof(Real) == 8) {
-                    const Real dE = (-e + (1 - rE * e) * SE) / tauE;
-                    const Real dI = (-in + (1 - rI * in) * SI) / tauI;
-                    const Real dA = (in * (e - rhoE)) / tau_ip;
+                    // (the divisions by the time constants as a product with the reciprocal plus one
+                    // correction step: the quotient to within an ulp, without the IEEE sequence)
+                    auto qdiv = [](double x, double y, double iy) {
+                        const double q = x * iy;
+                        return __builtin_fma(__builtin_fma(-y, q, x), iy, q);
+                    };
+                    const Real dE = qdiv(-e + (1 - rE * e) * SE, tauE, itauE);
+                    const Real dI = qdiv(-in + (1 - rI * in) * SI, tauI, itauI);
+                    const Real dA = qdiv(in * (e - rhoE), tau_ip, itau_ip);
                     E[u][r] = e + dt * dE;
                     I[u][r] = in + dt * dI;
                     A[u][r].add(dt * dA);

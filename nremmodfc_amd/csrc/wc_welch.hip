@@ -27,6 +27,10 @@ constexpr int kFFT = kSeg / 2; // packed complex length
 constexpr int kBins = kFFT + 1;
 constexpr int kThreads = 256;
 constexpr int kBinsPerThread = (kBins + kThreads - 1) / kThreads;  // 8
+#ifndef WC_WELCH_F64_THREADS
+#define WC_WELCH_F64_THREADS 768  // (1024 spills at the 128-VGPR cap; 768: 100 VGPRs, 12 waves)
+#endif
+constexpr int kWelchF64Threads = WC_WELCH_F64_THREADS;
 
 template <typename R> struct cx { R re, im; };
 template <typename R> __device__ __forceinline__ cx<R> cmul(cx<R> a, cx<R> b) {
@@ -110,10 +114,10 @@ __device__ __forceinline__ void stage(const cx<R>* __restrict__ x, cx<R>* __rest
     for (int s = 0; s < RAD; ++s) y[j + s * p] = U[s];
 }
 
-template <typename R, int RAD>
+template <typename R, int RAD, int T = kThreads>
 __device__ __forceinline__ void run_stage(cx<R>* const* src, cx<R>* const* dst, int p, const double* tw) {
     constexpr int nb = kFFT / RAD;
-    for (int idx = threadIdx.x; idx < kG<R> * nb; idx += kThreads) {
+    for (int idx = threadIdx.x; idx < kG<R> * nb; idx += T) {
         const int g = idx / nb, i = idx % nb;
         stage<R, RAD>(src[g], dst[g], p, i, tw);
     }
@@ -130,11 +134,14 @@ struct WelchArgs {
     double* acc;       // [B][kBins] running sum over nodes and segments of |X_k|^2
 };
 
-template <typename R>
-__global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
+// T threads per workgroup: 256 for the fp32 fallback; 768 for fp64 (kWelchF64Threads), whose
+// 128 KB of LDS allow one workgroup per CU -- 12 waves instead of 4 to hide its LDS and memory latency
+template <typename R, int T = kThreads>
+__global__ void __launch_bounds__(T) welch_kernel(const WelchArgs a) {
+    constexpr int kW = T / 64, kBpt = (kBins + T - 1) / T;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cx<R>* base = reinterpret_cast<cx<R>*>(smem);  // [kG][2][kFFT]
-    R* red = reinterpret_cast<R*>(base + 2 * kG<R> * kFFT);  // [4 waves][kG]
+    R* red = reinterpret_cast<R*>(base + 2 * kG<R> * kFFT);  // [kW waves][kG]
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     const R* E = static_cast<const R*>(a.E);
@@ -145,9 +152,9 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
         buf0[g] = base + (2 * g) * kFFT;
         buf1[g] = base + (2 * g + 1) * kFFT;
     }
-    double acc[kBinsPerThread];
+    double acc[kBpt];
 #pragma unroll
-    for (int j = 0; j < kBinsPerThread; ++j) acc[j] = 0.0;
+    for (int j = 0; j < kBpt; ++j) acc[j] = 0.0;
 
     for (int n0 = 0; n0 < a.N; n0 += kG<R>) {
         // ---- stage the raw segments (as reals) and their sums ----
@@ -165,7 +172,7 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
                     const int64_t q = ts / a.slot, r = ts % a.slot;
                     const int len = (int)min((int64_t)(kSeg - t), a.slot - r);
                     const R* src = col + (q % a.nslots) * a.slot + r;
-                    for (int i = tid; i < len; i += kThreads) {
+                    for (int i = tid; i < len; i += T) {
                         const R v = src[i];
                         xr[t + i] = v;
                         part[g] += v;
@@ -173,7 +180,7 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
                     t += len;
                 }
             } else {
-                for (int t = tid; t < kSeg; t += kThreads) xr[t] = 0;
+                for (int t = tid; t < kSeg; t += T) xr[t] = 0;
             }
         }
         // block reduction of the kG sums (wave shuffles, then 4 partials per g)
@@ -187,12 +194,16 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
         R mean[kG<R>];
 #pragma unroll
         for (int g = 0; g < kG<R>; ++g)
-            mean[g] = (red[g] + red[kG<R> + g] + red[2 * kG<R> + g] + red[3 * kG<R> + g]) / (R)kSeg;
+        {
+            R sum = 0;
+            for (int wv = 0; wv < kW; ++wv) sum += red[wv * kG<R> + g];  // (wave order: deterministic)
+            mean[g] = sum / (R)kSeg;
+        }
         // ---- detrend, periodic Hann window, pack z[n] = x[2n] + i x[2n+1] (in place) ----
 #pragma unroll
         for (int g = 0; g < kG<R>; ++g) {
             cx<R>* z = buf0[g];
-            for (int m = tid; m < kFFT; m += kThreads) {
+            for (int m = tid; m < kFFT; m += T) {
                 const cx<R> v = z[m];
                 const R w0 = (R)(0.5 - 0.5 * a.tw[2 * (2 * m)]);
                 const R w1 = (R)(0.5 - 0.5 * a.tw[2 * (2 * m + 1)]);
@@ -201,15 +212,15 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
         }
         __syncthreads();
         // ---- Stockham 2000 = 5 * 5 * 5 * 4 * 4 ----
-        run_stage<R, 5>(buf0, buf1, 1, a.tw);
-        run_stage<R, 5>(buf1, buf0, 5, a.tw);
-        run_stage<R, 5>(buf0, buf1, 25, a.tw);
-        run_stage<R, 4>(buf1, buf0, 125, a.tw);
-        run_stage<R, 4>(buf0, buf1, 500, a.tw);
+        run_stage<R, 5, T>(buf0, buf1, 1, a.tw);
+        run_stage<R, 5, T>(buf1, buf0, 5, a.tw);
+        run_stage<R, 5, T>(buf0, buf1, 25, a.tw);
+        run_stage<R, 4, T>(buf1, buf0, 125, a.tw);
+        run_stage<R, 4, T>(buf0, buf1, 500, a.tw);
         // ---- unpack X_k = (Z_k + conj Z_{-k})/2 - i/2 W^k (Z_k - conj Z_{-k}), |X_k|^2 ----
 #pragma unroll
-        for (int j = 0; j < kBinsPerThread; ++j) {
-            const int k = tid + j * kThreads;
+        for (int j = 0; j < kBpt; ++j) {
+            const int k = tid + j * T;
             if (k < kBins) {
 #pragma unroll
                 for (int g = 0; g < kG<R>; ++g) {
@@ -229,8 +240,8 @@ __global__ void __launch_bounds__(kThreads) welch_kernel(const WelchArgs a) {
         __syncthreads();  // buffers reused by the next node group
     }
 #pragma unroll
-    for (int j = 0; j < kBinsPerThread; ++j) {
-        const int k = tid + j * kThreads;
+    for (int j = 0; j < kBpt; ++j) {
+        const int k = tid + j * T;
         if (k < kBins) a.acc[(int64_t)b * kBins + k] += acc[j];
     }
 }
@@ -927,11 +938,12 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
         WelchArgs a{B, N, E, ld, slot, nslots, seg0 + (int64_t)sg * (kSeg / 2), wave ? nseg : 1,
                     static_cast<const double*>(workspace), acc};
         if (e_f64) {
-            const size_t lds = (size_t)2 * kG<double> * kFFT * sizeof(cx<double>) + 4 * kG<double> * sizeof(double);
-            hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<double>,
+            constexpr int T = kWelchF64Threads;
+            const size_t lds = (size_t)2 * kG<double> * kFFT * sizeof(cx<double>) + (T / 64) * kG<double> * sizeof(double);
+            hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<double, T>,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
-            hipLaunchKernelGGL(welch_kernel<double>, dim3(B), dim3(kThreads), lds, st, a);
+            hipLaunchKernelGGL((welch_kernel<double, T>), dim3(B), dim3(T), lds, st, a);
         } else if (wave) {
 #if WC_WELCH_PAIR
             if (nseg != 1) return wc_set_err(WC_EINVAL, "wc_welch_accumulate: the pair build takes one segment");
