@@ -28,9 +28,11 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
 }
 
+// one v_mad_u64_u32 for hi:lo.  Written in C, not inline asm: the compiler picks the carry-out
+// SGPR pair itself, whereas an asm block writing vcc got an s_nop after every multiply (18 per
+// wave-step in the C3 integrator)
 __device__ __forceinline__ void mul_wide(uint32_t a, uint32_t m, uint32_t& hi, uint32_t& lo) {
-    uint64_t r;
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(r) : "v"(a), "s"(m) : "vcc");  // one op for hi:lo
+    const uint64_t r = (uint64_t)a * (uint64_t)m;
     hi = (uint32_t)(r >> 32);
     lo = (uint32_t)r;
 }
