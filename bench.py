@@ -157,18 +157,21 @@ def run_workload(sc, G, S, keys, p, args, dev, dist, steps, warmup):
     B = len(keys)
     C = B * N
     bt = Batch(sc, G, S, keys, p, precision=args.precision, device=dev)
-    R, CH, NSLOT = 20, 1000, 6           # record every 20 steps; 1000-sample chunks; 6-slot ring (Welch pairs)
+    R, CH = 20, 1000                     # record every 20 steps; 1000-sample integrator chunks (20,000 Euler steps)
     WELCH_SEG = 4000                     # nperseg (whole_sweep_both.py:90), hop WELCH_SEG / 2
-    LD = CH * NSLOT
-    EULER = CH * R                       # Euler steps per chunk
     CHUNKS = 2                           # chunks per bench step (one Welch segment per step: a launch of two
                                          # overlapping segments every other step, as the sweep pipeline runs them)
+    SLOT, NSLOT = CH * CHUNKS, 3         # the 6000-sample Welch ring in 2000-sample slots: one BOLD pass per step
+    LD = SLOT * NSLOT                    # (slots start 8000 B apart, a multiple of 64 B: 1000-sample slots put every
+                                         # other one 32 B off a line and its node-major rows cost ~0.55 ms more per
+                                         # chunk, profiles/r04_ab/ring_align.log)
+    EULER = CH * R                       # Euler steps per chunk
     n_total = (warmup + steps) * CHUNKS * CH + NEQ
     ring = torch.empty(C * LD, dtype=bt.rec_dtype, device=dev)
-    # fp32 + consumers: the integrator writes each chunk time-major, the BOLD pass transposes it
-    # into the node-major Welch ring (the sweep pipeline's layout, nremmodfc_amd/pipeline.py)
+    # fp32 + consumers: the integrator writes each step's two chunks time-major, the BOLD pass transposes
+    # them into the node-major Welch ring (the sweep pipeline's layout, nremmodfc_amd/pipeline.py)
     # (--sde-only records the same way, time-major, so it times exactly the pipeline's integrator work)
-    tmaj = torch.empty(CH * C, dtype=bt.rec_dtype, device=dev) if args.precision == "f32" else None
+    tmaj = torch.empty(SLOT * C, dtype=bt.rec_dtype, device=dev) if args.precision == "f32" else None
     bold = welch = None
     if not args.sde_only:
         bold = BoldStream(C, max(n_total, 300_000), NEQ, 1000, p.dt * p.downsamp, dev)
@@ -188,33 +191,33 @@ def run_workload(sc, G, S, keys, p, args, dev, dist, steps, warmup):
         ev[name].append((e0, e1))
 
     def step():
-        """2000 recorded samples (40,000 Euler steps) of every simulation: integrate into the ring,
-        stream BOLD over each 1000-sample chunk, one 4000-sample Welch segment (every other step one
-        launch of the last two segments, as nremmodfc_amd/pipeline.py does)."""
-        for _ in range(CHUNKS):
-            k = state["k"]
-            slot = k % NSLOT
+        """2000 recorded samples (40,000 Euler steps) of every simulation: integrate two 1000-sample
+        chunks, stream BOLD over the 2000 samples into their ring slot, one 4000-sample Welch segment
+        (every other step one launch of the last two segments, as nremmodfc_amd/pipeline.py does)."""
+        slot = (state["k"] // CHUNKS) % NSLOT
+        for h in range(CHUNKS):
             if tmaj is not None:
-                timed("sde", lambda: bt.integrate(EULER, 2.0, R, tmaj))
-                if bold is not None:
-                    timed("bold", lambda: bold.feed(tmaj, CH, e_ld=0, copy=ring, copy_ld=LD, copy_offset=slot * CH))
+                timed("sde", lambda: bt.integrate(EULER, 2.0, R, tmaj[h * CH * C:]))
             else:
-                timed("sde", lambda: bt.integrate(EULER, 2.0, R, ring[slot * CH:], rec_ld=LD))
-                if bold is not None:
-                    timed("bold", lambda: bold.feed(ring, CH, e_ld=LD, offset=slot * CH))
-            state["k"] = k = k + 1
+                timed("sde", lambda: bt.integrate(EULER, 2.0, R, ring[slot * SLOT + h * CH:], rec_ld=LD))
+        if bold is not None:
+            if tmaj is not None:
+                timed("bold", lambda: bold.feed(tmaj, SLOT, e_ld=0, copy=ring, copy_ld=LD, copy_offset=slot * SLOT))
+            else:
+                timed("bold", lambda: bold.feed(ring, SLOT, e_ld=LD, offset=slot * SLOT))
+        state["k"] += CHUNKS
         # the segment ending at this step's last sample: held for one step and launched with the next
         # one (two per launch, as the pipeline does); flush_welch() launches a held one alone
         if welch is not None and state["k"] * CH >= WELCH_SEG:
             if state["pending"]:
                 k = state["k"]
-                timed("welch", lambda: welch.accumulate(ring, LD, CH, NSLOT, k * CH - WELCH_SEG - WELCH_SEG // 2, nseg=2))
+                timed("welch", lambda: welch.accumulate(ring, LD, SLOT, NSLOT, k * CH - WELCH_SEG - WELCH_SEG // 2, nseg=2))
             state["pending"] = not state["pending"]
 
     def flush_welch():
         if welch is not None and state["pending"]:
             k = state["k"]
-            timed("welch1", lambda: welch.accumulate(ring, LD, CH, NSLOT, k * CH - WELCH_SEG))
+            timed("welch1", lambda: welch.accumulate(ring, LD, SLOT, NSLOT, k * CH - WELCH_SEG))
             state["pending"] = False
 
     for _ in range(warmup):
@@ -241,6 +244,8 @@ def run_workload(sc, G, S, keys, p, args, dev, dist, steps, warmup):
     kern = {k: (sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None) for k, v in ev.items()}
     if kern["welch"] is not None:
         kern["welch"] /= 2  # ms per segment (each launch takes two)
+    if kern["bold"] is not None:
+        kern["bold"] /= CHUNKS  # ms per 1000-sample chunk (each pass takes a step's two)
     kern.pop("welch1")  # (a lone last segment of an odd step count: timed in the step, not reported)
     return elapsed, kern
 
@@ -435,7 +440,7 @@ def main():
                                 "C5: 1000-node synthetic connectome, 2,500 sims of the (G,sigma) grid per GPU; ")
                                + "one step = 2000 recorded samples (40,000 Euler steps, tau_ip=2) of every simulation"
                                + ("" if args.sde_only else
-                                  " + streamed BOLD/band-pass of both 1000-sample chunks + one Welch segment"),
+                                  " + streamed BOLD/band-pass of the 2000 samples + one Welch segment"),
                    "sims_per_gpu": B, "sims_total": B_all, "nodes": N, "euler_steps_per_step": EULER * CHUNKS,
                    "record_every": R, "parallelism": f"sims sharded x{world} ({args.scaling} scaling)"},
         "roofline": roof,

@@ -641,6 +641,9 @@ constexpr int kPersistRetry = 1;                      // run_persistent: coopera
 #ifndef WC_PPAIR
 #define WC_PPAIR 1
 #endif
+#ifndef WC_PEARLY
+#define WC_PEARLY 1  // the next pair's operand loads issued before the pair's barrier
+#endif
 // K chunks of the connectome tile kept in LDS (112 KB of the 512 KB streamed per step; 8 chunks
 // = 128 KB before the image stages were paired, WC_PPAIR)
 constexpr int kPRes = WC_PPAIR ? 7 : 8;
@@ -916,6 +919,20 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             stage_put(ps, h, tid, rb[h][0]);
             if (tid < 128) stage_put(ps, h, 512 + tid, rb[h][1]);
         }
+#if WC_PEARLY
+        // the next pair's loads issued before the barrier (the staged registers are free once
+        // their ds_writes have issued; the A operands of this pair taken first: each wave reads
+        // only its own ldsA slice)
+        const f16x8 a00 = c < res ? ldsA[c][w][0][lane] : fa[0][0];
+        const f16x8 a01 = c < res ? ldsA[c][w][1][lane] : fa[0][1];
+        const f16x8 a10 = c + 1 < res ? ldsA[c + 1][w][0][lane] : fa[1][0];
+        const f16x8 a11 = c + 1 < res ? ldsA[c + 1][w][1][lane] : fa[1][1];
+        if (c + 2 < g.NC) {
+            load_chunk(c + 2, 0, buf);
+            load_chunk(c + 3, 1, buf);
+        }
+        __syncthreads();
+#else
         __syncthreads();
         const f16x8 a00 = c < res ? ldsA[c][w][0][lane] : fa[0][0];
         const f16x8 a01 = c < res ? ldsA[c][w][1][lane] : fa[0][1];
@@ -925,6 +942,7 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             load_chunk(c + 2, 0, buf);
             load_chunk(c + 3, 1, buf);
         }
+#endif
         mfma_chunk(c, a00, a01, ldsB[ps][0], acc);
         mfma_chunk(c + 1, a10, a11, ldsB[ps][1], acc);
     };

@@ -17,6 +17,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <type_traits>
 #include "wc_common.h"
 
 namespace {
@@ -263,9 +264,9 @@ constexpr int kWv = 4;       // waves (columns in flight) per simulation
 constexpr int kSimsWg = 2;   // simulations per workgroup
 constexpr int kLaneBins = (kBins + 63) / 64;  // 32
 #ifndef WC_WELCH_PF_EARLY
-#define WC_WELCH_PF_EARLY 7
+#define WC_WELCH_PF_EARLY 8  // (all of them; clipped to the row count, and even under WC_WELCH_X4)
 #endif
-constexpr int kPfEarly = WC_WELCH_PF_EARLY;  // rows of the next column fetched right after stage 1
+constexpr int kPfEarly = WC_WELCH_PF_EARLY;  // rows of the next column fetched right after stage 1 (min'd with kXR below)
 // per-stage twiddle tables: entry (k, r) = T^(r k TS) at base + (r - 1) P + k (r-major: the
 // lanes of a row read consecutive k, conflict-free; r is an immediate offset)
 // (stages 5 x 5 x 5 x 16; the first has no twiddles)
@@ -359,9 +360,21 @@ __device__ __forceinline__ void butterfly(const f2 (&u)[RAD], f2 (&U)[RAD]) {
     }
 }
 
-template <int RAD, int P>
-__device__ __forceinline__ void write_rows(f2* z, f2 (&u)[Rows<RAD, P>::NB][RAD], int lane) {
-    using R = Rows<RAD, P>;
+#ifndef WC_WELCH_X4
+#define WC_WELCH_X4 1  // stage-1 points fetched as 16-B pairs (two butterflies per lane and load)
+#endif
+// stage 1 under WC_WELCH_X4: lane l holds butterflies 2l + j + 128 p (rows q = 2p + j, p < 4), so
+// one 16-B load brings the points of rows 2p and 2p + 1; rows 6 and 7 are owned by lanes 0..7
+// only (the others re-read points 398, 399 and write nothing)
+struct Rows1x4 {
+    static constexpr int S = kFFT / 5, NB = 8;
+    __device__ static int idx(int lane, int q) { return min(2 * lane + (q & 1) + 128 * (q >> 1), S - 1); }
+    __device__ static bool own(int lane, int q) { return q < 6 || 2 * lane + (q & 1) + 128 * (q >> 1) < S; }
+    __device__ static int pair_base(int lane, int p) { return min(2 * lane + 128 * p, S - 2); }  // even
+};
+
+template <typename R, int RAD, int P>
+__device__ __forceinline__ void write_rows_t(f2* z, f2 (&u)[R::NB][RAD], int lane) {
 #pragma unroll
     for (int q = 0; q < R::NB; ++q) {
         const int i = R::idx(lane, q), k = i % P;
@@ -375,15 +388,25 @@ __device__ __forceinline__ void write_rows(f2* z, f2 (&u)[Rows<RAD, P>::NB][RAD]
     }
 }
 
+template <int RAD, int P>
+__device__ __forceinline__ void write_rows(f2* z, f2 (&u)[Rows<RAD, P>::NB][RAD], int lane) {
+    write_rows_t<Rows<RAD, P>, RAD, P>(z, u, lane);
+}
+
 // stage 1 (radix 5, no twiddles) fed from registers: x[q][r] = packed point i + 400 r of
 // the raw column; the column mean (constant detrend) and the periodic Hann window
 // w(t) = 0.5 - 0.5 cos(2 pi t / 4000) are applied on the way in
-__device__ __forceinline__ void wstage1(f2* z, f2 (&x)[7][5], const f2* __restrict__ hann, int lane) {
-    using R = Rows<5, 1>;
+using Rows1 = std::conditional_t<WC_WELCH_X4 != 0, Rows1x4, Rows<5, 1>>;
+constexpr int kXR = Rows1::NB;  // stage-1 rows per lane: 8 (16-B pairs) or 7
+constexpr int kPf = kPfEarly < kXR ? kPfEarly : kXR;
+static_assert(!WC_WELCH_X4 || kPf % 2 == 0, "16-B pair fetch: an even number of early rows");
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void wstage1(f2* z, f2 (&x)[kXR][5], const f2* __restrict__ hann, int lane) {
+    using R = Rows1;
     float part = 0.f;
-    f2 hw[7][5];
+    f2 hw[kXR][5];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) {
+    for (int q = 0; q < kXR; ++q) {
         const int i = R::idx(lane, q);
 #pragma unroll
         for (int r = 0; r < 5; ++r) {
@@ -391,6 +414,14 @@ __device__ __forceinline__ void wstage1(f2* z, f2 (&x)[7][5], const f2* __restri
             // (w(2m), w(2m+1)); unsigned byte offset: the saddr form of the load
 #if defined(WC_WELCH_DIAG_NOHANN)  // (ablation builds only: timing without the window loads, wrong PSD)
             hw[q][r] = (f2){1.0f, 1.0f};
+            (void)i;
+#elif WC_WELCH_X4
+            if ((q & 1) == 0) {  // the window of rows q, q + 1 in one 16-B load
+                const f4v w4 = *reinterpret_cast<const f4v*>(
+                    reinterpret_cast<const char*>(hann) + (unsigned)(R::pair_base(lane, q >> 1) + r * R::S) * 8u);
+                hw[q][r] = (f2){w4.x, w4.y};
+                hw[q + 1][r] = (f2){w4.z, w4.w};
+            }
             (void)i;
 #else
             hw[q][r] = *reinterpret_cast<const f2*>(reinterpret_cast<const char*>(hann) + (unsigned)(i + r * R::S) * 8u);
@@ -400,10 +431,10 @@ __device__ __forceinline__ void wstage1(f2* z, f2 (&x)[7][5], const f2* __restri
     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
     const float mean = part / (float)kSeg;
 #pragma unroll
-    for (int q = 0; q < 7; ++q)
+    for (int q = 0; q < kXR; ++q)
 #pragma unroll
         for (int r = 0; r < 5; ++r) x[q][r] = (x[q][r] - mean) * hw[q][r];
-    write_rows<5, 1>(z, x, lane);
+    write_rows_t<R, 5, 1>(z, x, lane);
     wave_sync();
 }
 
@@ -553,9 +584,27 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
     // (x[q][r] = packed point i + 400 r, i = lane + 64 q); the next column is fetched
     // while the current one is transformed (branch-free: the clamped lanes of row 6
     // re-read a valid point, and a wave's last column re-fetches itself, an L2 hit)
-    f2 x[7][5];
+    f2 x[kXR][5];
     const int64_t bc = (int64_t)min(b, a.B - 1) * a.N;
     // (uniform column base + 32-bit unsigned lane offset: the saddr form of global_load)
+#if WC_WELCH_X4
+    // rows 2p, 2p + 1 from one 16-B load of points i0, i0 + 1 (i0 even: the four samples sit in one
+    // aligned group, which the ring's wrap never splits: seg0, L and the slot length are multiples of 4)
+#define WELCH_FETCH(n, Q0, Q1, LN)                                                             \
+    {                                                                                          \
+        const float* col_ = E + (bc + (n)) * a.ld;                                             \
+        _Pragma("unroll") for (int p = (Q0) / 2; p < (Q1) / 2; ++p) {                          \
+            const int i_ = Rows1x4::pair_base(LN, p);                                          \
+            _Pragma("unroll") for (int r = 0; r < 5; ++r) {                                    \
+                unsigned o_ = baseB + 8u * (unsigned)(i_ + 400 * r);                           \
+                o_ = min(o_, o_ - LB);                                                         \
+                const f4v v_ = *reinterpret_cast<const f4v*>(reinterpret_cast<const char*>(col_) + o_); \
+                x[2 * p][r] = (f2){v_.x, v_.y};                                                \
+                x[2 * p + 1][r] = (f2){v_.z, v_.w};                                            \
+            }                                                                                  \
+        }                                                                                      \
+    }
+#else
 #define WELCH_FETCH(n, Q0, Q1, LN)                                                             \
     {                                                                                          \
         const float* col_ = E + (bc + (n)) * a.ld;                                             \
@@ -568,7 +617,8 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
             }                                                                                  \
         }                                                                                      \
     }
-    WELCH_FETCH(min(c0, a.N - 1), 0, 7, lane);
+#endif
+    WELCH_FETCH(min(c0, a.N - 1), 0, kXR, lane);
     {  // twiddle tables into LDS: T^0..T^2000 and the stage tables (the pad entry is never read)
         const f2* src = reinterpret_cast<const f2*>(twg);
         const f2* sst = reinterpret_cast<const f2*>(twg) + kSeg + kFFT;
@@ -591,7 +641,7 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
 #if defined(WC_WELCH_DIAG_NOLOAD)  // (ablation builds only: tools/dbg/welch_variants.sh)
         (void)nn;
 #else
-        WELCH_FETCH(nn, 0, kPfEarly, ln);
+        WELCH_FETCH(nn, 0, kPf, ln);
 #endif
 #if defined(WC_WELCH_DIAG_NOFFT)
         {
@@ -599,12 +649,12 @@ __global__ void __launch_bounds__(kWv * kSimsWg * 64, 1) welch_wave_kernel(const
             acc[0][0] += v.x;
             acc[0][1] += v.y;
         }
-        WELCH_FETCH(nn, kPfEarly, 7, ln);
+        WELCH_FETCH(nn, kPf, kXR, ln);
 #else
         wstage<5, 5, kTb2>(z, Ts, ln);
         wstage<5, 25, kTb3>(z, Ts, ln);
 #if !defined(WC_WELCH_DIAG_NOLOAD)
-        WELCH_FETCH(nn, kPfEarly, 7, ln);  // (the rest of the next column: fewer live registers through the stages)
+        WELCH_FETCH(nn, kPf, kXR, ln);  // (the rest of the next column: fewer live registers through the stages)
 #endif
         wstage_last_unpack(z, Ts, Tu, acc, ln);
 #endif

@@ -12,12 +12,15 @@ do one simulation at a time:
   utils.kuramoto(BOLD), np.mean(sFC)                                  -> wc_hilbert_phase + wc_fc_metrics
 
 The recorded phase runs in chunks of `chunk_samples` samples (20 Euler steps
-each).  The integrator writes each chunk time-major ([chunk][C] fp32, 7.2 GB
-at 20,000 x 90: full-line stores); the BOLD stream consumes it right away and
-in the same pass writes it node-major into one slot of a 6-slot ring ([C][6*chunk]
-fp32, 43.2 GB), from which the completed 4000-sample Welch segments are
-transformed two at a time (one launch reads their shared half once from HBM) --
-the 648 MB/simulation trajectory of the reference never exists.
+each; 2000 by default).  The integrator writes each chunk time-major ([chunk][C]
+fp32, 14.4 GB at 20,000 x 90: full-line stores); the BOLD stream consumes it
+right away and in the same pass writes it node-major into one slot of a 6000-sample
+ring ([C][6000] fp32, 43.2 GB), from which the completed 4000-sample Welch
+segments are transformed two at a time (one launch reads their shared half once
+from HBM) -- the 648 MB/simulation trajectory of the reference never exists.
+(2000-sample slots start 8000 B apart, a multiple of 64 B; with 1000-sample slots
+every other slot sits 32 B off a line and its node-major rows cost the BOLD pass
+~0.55 ms more per 1000 samples at C3, profiles/r04_ab/ring_align.log.)
 """
 from __future__ import annotations
 
@@ -60,7 +63,7 @@ class SweepResult:
         return out
 
 
-def check_supported(N, schedule: Schedule = None, chunk_samples: int = 1000):
+def check_supported(N, schedule: Schedule = None, chunk_samples: int = 2000):
     """Raise before any device work if the pipeline cannot produce every output for
     an N-node connectome on this schedule (the epilogue's limits included)."""
     sch = schedule or Schedule()
@@ -73,7 +76,7 @@ def check_supported(N, schedule: Schedule = None, chunk_samples: int = 1000):
 
 
 def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedule: Schedule = None,
-              params: WCParams = None, precision: str = F32, chunk_samples: int = 1000,
+              params: WCParams = None, precision: str = F32, chunk_samples: int = 2000,
               bold_downsamp: int = 1000, max_launch_steps: int = 500_000, want_fc=False, want_bold=False,
               device="cuda", progress=None, init_state: Optional[Dict[str, np.ndarray]] = None) -> SweepResult:
     """Run B simulations end to end and return the reference's per-simulation outputs.
