@@ -310,6 +310,26 @@ __device__ __forceinline__ f2 cmulv(f2 u, f2 w) {  // u * w in two packed ops
         : "=v"(r) : "v"(u), "v"(w), "v"(t));
     return r;
 }
+// two independent products with their instructions interleaved: a v_pk_* op that reads the result of
+// the one right before it needs a wait state on gfx950 (an s_nop when nothing independent sits between)
+__device__ __forceinline__ void cmulv2(f2& u0, f2 w0, f2& u1, f2 w1) {
+    f2 t0, t1, r0, r1;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t0) : "v"(u0), "v"(w0));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t1) : "v"(u1), "v"(w1));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r0) : "v"(u0), "v"(w0), "v"(t0));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r1) : "v"(u1), "v"(w1), "v"(t1));
+    u0 = r0;
+    u1 = r1;
+}
+// u[r] *= w[r - 1] for r = 1 .. K - 1, two products at a time
+template <int K>
+__device__ __forceinline__ void cmul_rows(f2 (&u)[K], const f2 (&w)[K - 1]) {
+#pragma unroll
+    for (int r = 1; r + 1 < K; r += 2) cmulv2(u[r], w[r - 1], u[r + 1], w[r]);
+    if constexpr ((K - 1) % 2) u[K - 1] = cmulv(u[K - 1], w[K - 2]);
+}
 __device__ __forceinline__ f2 add_mi(f2 a, f2 d) {  // a - i d = (a.x + d.y, a.y - d.x)
     f2 r;
     asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(d));
@@ -463,8 +483,7 @@ __device__ __forceinline__ void wstage(f2* z, const f2* Ts, int lane) {
             for (int r = 1; r < RAD; ++r)
                 tw[(q + 1) & 1][r - 1] = ldsr(Ts + TB + R::idx(lane, q + 1) % P + (r - 1) * P);
         }
-#pragma unroll
-        for (int r = 1; r < RAD; ++r) u[q][r] = cmulv(u[q][r], tw[q & 1][r - 1]);
+        cmul_rows<RAD>(u[q], tw[q & 1]);
     }
     write_rows<RAD, P>(z, u, lane);
     wave_sync();
@@ -481,14 +500,10 @@ __device__ __forceinline__ void dft16(f2 (&u)[16]) {
         butterfly<4>(in, v[r2]);
     }
     // W16^j = (cos, -sin)(2 pi j / 16): j = r2 s1 in {1, 2, 3, 4, 6, 9}
-    v[1][1] = cmulv(v[1][1], (f2){c, -d});
-    v[1][2] = cmulv(v[1][2], (f2){h, -h});
-    v[1][3] = cmulv(v[1][3], (f2){d, -c});
-    v[2][1] = cmulv(v[2][1], (f2){h, -h});
-    v[2][2] = cmulv(v[2][2], (f2){0.f, -1.f});
-    v[2][3] = cmulv(v[2][3], (f2){-h, -h});
-    v[3][1] = cmulv(v[3][1], (f2){d, -c});
-    v[3][2] = cmulv(v[3][2], (f2){-h, -h});
+    cmulv2(v[1][1], (f2){c, -d}, v[1][2], (f2){h, -h});
+    cmulv2(v[1][3], (f2){d, -c}, v[2][1], (f2){h, -h});
+    cmulv2(v[2][2], (f2){0.f, -1.f}, v[2][3], (f2){-h, -h});
+    cmulv2(v[3][1], (f2){d, -c}, v[3][2], (f2){-h, -h});
     v[3][3] = cmulv(v[3][3], (f2){-c, d});
 #pragma unroll
     for (int s1 = 0; s1 < 4; ++s1) {
@@ -531,27 +546,45 @@ __device__ __forceinline__ void wstage_last_unpack(const f2* z, const f2* Ts, co
     f2 tw[2][15], tu[16];
 #pragma unroll
     for (int r = 1; r < 16; ++r) tw[0][r - 1] = ldsr(Ts + kTb4 + (r - 1) * 125 + rows[0]);
-#pragma unroll
-    for (int r = 1; r < 16; ++r) u[0][r] = cmulv(u[0][r], tw[0][r - 1]);
+    cmul_rows<16>(u[0], tw[0]);
 #pragma unroll
     for (int r = 1; r < 16; ++r) tw[1][r - 1] = ldsr(Ts + kTb4 + (r - 1) * 125 + rows[1]);
     dft16(u[0]);
-#pragma unroll
-    for (int r = 1; r < 16; ++r) u[1][r] = cmulv(u[1][r], tw[1][r - 1]);
+    cmul_rows<16>(u[1], tw[1]);
 #pragma unroll
     for (int s2i = 0; s2i < 16; ++s2i) tu[s2i] = ldsr(Tu + m + 125 * s2i);
     dft16(u[1]);
+    // two bins at a time, their instructions interleaved (no v_pk_* right behind its producer; the
+    // same operations on every value)
 #pragma unroll
-    for (int s2i = 0; s2i < 16; ++s2i) {
-        const f2 Zk = u[0][s2i];
-        const f2 Zc = m == 0 ? u[0][(16 - s2i) & 15] : u[1][15 - s2i];
-        f2 sv, dv;
-        asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv) : "v"(Zk), "v"(Zc));
-        asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv) : "v"(Zk), "v"(Zc));
-        const f2 pv = cmulv(dv, tu[s2i]);
-        const f2 xa = add_mi(sv, pv), xb = sub_mi(sv, pv);
-        acc[s2i][0] = sq_acc(xa.x, sq_acc(xa.y, acc[s2i][0]));
-        acc[s2i][1] = sq_acc(xb.x, sq_acc(xb.y, acc[s2i][1]));
+    for (int s2i = 0; s2i < 16; s2i += 2) {
+        f2 sv[2], dv[2], pv[2], xa[2], xb[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int si = s2i + k;
+            const f2 Zk = u[0][si];
+            const f2 Zc = m == 0 ? u[0][(16 - si) & 15] : u[1][15 - si];
+            asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(sv[k]) : "v"(Zk), "v"(Zc));
+            asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(dv[k]) : "v"(Zk), "v"(Zc));
+        }
+        pv[0] = dv[0];
+        pv[1] = dv[1];
+        cmulv2(pv[0], tu[s2i], pv[1], tu[s2i + 1]);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) xa[k] = add_mi(sv[k], pv[k]);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) xb[k] = sub_mi(sv[k], pv[k]);
+        float t[2][2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            t[k][0] = sq_acc(xa[k].y, acc[s2i + k][0]);
+            t[k][1] = sq_acc(xb[k].y, acc[s2i + k][1]);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            acc[s2i + k][0] = sq_acc(xa[k].x, t[k][0]);
+            acc[s2i + k][1] = sq_acc(xb[k].x, t[k][1]);
+        }
     }
 }
 
