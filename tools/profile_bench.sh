@@ -57,7 +57,7 @@ sig = {"note": "rocprofv3 --pmc passes of the same bench run (tools/profile_benc
                "wave_cycle_split: SQ_WAIT_ANY (parked on s_waitcnt/barrier), SQ_WAIT_INST_ANY (issue stall), "
                "SQ_ACTIVE_INST_ANY (issuing), fractions of SQ_WAVE_CYCLES."}
 C = 20000 * 90
-for name, sub, units, per in (("bold_steady_copy", "bold_chunk_kernel<float, true, true, true>", C * 1000.0 / 64, "wave-sample"),
+for name, sub, units, per in (("bold_steady_copy", "bold_chunk_kernel<float, true, true, true>", C * 2000.0 / 64, "wave-sample"),  # (one pass per 2000 samples)
                               ("welch", "welch_wave_kernel", 2.0 * C, "column-segment")):  # (two segments per launch)
     a = summary("gpurun_out/prof/sq", sub)
     b = summary("gpurun_out/prof/sq2", sub)
