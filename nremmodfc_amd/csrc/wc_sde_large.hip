@@ -736,8 +736,9 @@ __host__ __device__ __forceinline__ uint32_t pimg_unit16(const PGeo& g, int c, i
     return (uint32_t)((((size_t)c * g.SBp + sb) * kPT + t) * 2 + h);
 }
 
-// DIAG (timing ablations only, diag build, WCSDE_PERSISTENT=2..5; results are wrong): 1 = no MFMA, 2 = no
-// epilogue arithmetic, 3 = no K-loop operand loads, 4 = no hand-off waits
+// DIAG (timing ablations only, diag build, WCSDE_PERSISTENT=2..7; results are wrong): 1 = no MFMA, 2 = no
+// epilogue arithmetic, 3 = no K-loop operand loads, 4 = no hand-off waits, 5 = no loads for the step's
+// first pair, 6 = no E-image loads (A rows still streamed)
 template <int DIAG = 0>
 __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a) {
     typedef __attribute__((ext_vector_type(4))) float f4;
@@ -876,6 +877,7 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             fa[slot][0] = ap[0];
             fa[slot][1] = ap[64];
         }
+        if (DIAG == 6) return;  // (ablation: no E-image loads, the A rows still streamed)
         const int xo = (int)(((buf * img_units + pimg_unit(g, c, sb, 0, 0)) * 64 + tid) * 16);
         rb[slot][0] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 16));
         if (tid < 128) rb[slot][1] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo + 512 * 16, 0, 16));
@@ -966,8 +968,10 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         f4 acc[kPT];
 #pragma unroll
         for (int t = 0; t < kPT; ++t) acc[t] = f4{0, 0, 0, 0};
-        load_chunk(0, 0, buf);
-        load_chunk(1, 1, buf);
+        if (DIAG != 5) {  // (ablation 5: the step's first pair from stale registers, no exposed round trip)
+            load_chunk(0, 0, buf);
+            load_chunk(1, 1, buf);
+        }
         for (int c = 0; c < g.NC; c += 2) {  // NC is a multiple of 4 (nodes padded to 128)
             if (WC_PPAIR) {
                 do_pair(c, buf, acc);
@@ -1067,7 +1071,7 @@ int cu_count_large() {
 // (libwcsde_diag.so) 2..5 select the timing ablations (wrong results).
 bool persistent_ok(int B, int N) {
     const char* env = getenv("WCSDE_PERSISTENT");
-    if (env && (env[0] < '1' || env[0] > '5')) return false;
+    if (env && (env[0] < '1' || env[0] > '7')) return false;
     const PGeo g = pgeometry(B, N);
     if (2 * (size_t)g.Np * g.Bp * 4 >= (size_t)INT32_MAX) return false;
     int occ = 0;
@@ -1116,6 +1120,8 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
         case '3': kern = (const void*)persist_kernel<2>; break;
         case '4': kern = (const void*)persist_kernel<3>; break;
         case '5': kern = (const void*)persist_kernel<4>; break;
+        case '6': kern = (const void*)persist_kernel<5>; break;
+        case '7': kern = (const void*)persist_kernel<6>; break;
         default: break;
     }
 #endif
