@@ -454,7 +454,26 @@ __device__ __forceinline__ void wstage1(f2* z, f2 (&x)[kXR][5], const f2* __rest
     for (int q = 0; q < kXR; ++q)
 #pragma unroll
         for (int r = 0; r < 5; ++r) x[q][r] = (x[q][r] - mean) * hw[q][r];
+#if WC_WELCH_X4
+    // butterflies i0, i0 + 1 write z[5 i0 .. 5 i0 + 9], 80 contiguous bytes per lane: five 16-B writes,
+    // conflict-free (lane stride 20 dwords) where ten 8-B ones at that stride met in pairs of lanes
+#pragma unroll
+    for (int p = 0; p < kXR / 2; ++p) {
+        f2 Ua[5], Ub[5];
+        butterfly<5>(x[2 * p], Ua);
+        butterfly<5>(x[2 * p + 1], Ub);
+        if (R::own(lane, 2 * p)) {
+            f4v* zz = reinterpret_cast<f4v*>(z + 5 * R::pair_base(lane, p));
+            zz[0] = (f4v){Ua[0].x, Ua[0].y, Ua[1].x, Ua[1].y};
+            zz[1] = (f4v){Ua[2].x, Ua[2].y, Ua[3].x, Ua[3].y};
+            zz[2] = (f4v){Ua[4].x, Ua[4].y, Ub[0].x, Ub[0].y};
+            zz[3] = (f4v){Ub[1].x, Ub[1].y, Ub[2].x, Ub[2].y};
+            zz[4] = (f4v){Ub[3].x, Ub[3].y, Ub[4].x, Ub[4].y};
+        }
+    }
+#else
     write_rows_t<R, 5, 1>(z, x, lane);
+#endif
     wave_sync();
 }
 
