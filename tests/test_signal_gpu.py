@@ -240,6 +240,25 @@ def test_pipeline_short_schedule_vs_oracle(cuda, sc90):
                 np.testing.assert_allclose(cols[name][b], v, rtol=1e-6, atol=1e-8, err_msg=name)
 
 
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_pipeline_chunk_length_invariance(cuda, sc90, prec):
+    """The recorded phase in 1000- or 2000-sample chunks (the default; ring slots 8000 B apart) gives
+    the same outputs bit for bit: the integrator is launch-chunking invariant, BOLD is fed in
+    either length, Welch takes the same segment pairs from a 6-slot or a 3-slot ring."""
+    from nremmodfc_amd.model import Schedule, sim_keys
+    from nremmodfc_amd.pipeline import run_sweep
+    sch = Schedule(n_trans1=200, n_trans2=2000, n_sim=200_000)  # T = 10,000 samples
+    G = np.array([0.16, 0.10, 0.22, 0.16, 0.30])
+    S = np.array([7.68, 7.50, 7.80, 7.88, 7.68])
+    keys = sim_keys([0, 1, 2, 3, 4], [0, 5, 9, 11, 3])
+    emp = {s: datasets.load_empfc(s) for s in datasets.STATES}
+    r1 = run_sweep(sc90, G, S, keys, emp, sch, precision=prec, chunk_samples=1000, want_bold=True)
+    r2 = run_sweep(sc90, G, S, keys, emp, sch, precision=prec, chunk_samples=2000, want_bold=True)
+    assert np.array_equal(r1.bold, r2.bold)
+    for name, v in r1.columns().items():
+        assert np.array_equal(v, r2.columns()[name]), name
+
+
 def test_pipeline_fc_ssim_vs_oracle(cuda, sc90):
     """Pathwise FC parity of the fp64 pipeline with the oracle while the two trajectories are still
     coherent: 2,200 transient + 400,000 recorded steps (18 BOLD samples), utils.py:48's
