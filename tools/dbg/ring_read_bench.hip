@@ -52,25 +52,29 @@ int main() {
         printf("alloc failed\n");
         return 1;
     }
-    hipMemset(ring, 0, (size_t)ncol * kLd * 4);
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
     int cus = 0;
-    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    if (hipMemset(ring, 0, (size_t)ncol * kLd * 4) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) {
+        printf("setup failed\n");
+        return 1;
+    }
     for (int rep = 0; rep < 3; ++rep) {
         for (int w = 0; w < 2; ++w) {
             for (int grid_mul : {1, 4}) {
                 const int grid = cus * grid_mul;
-                hipEventRecord(e0);
+                (void)hipEventRecord(e0);
                 if (w == 0)
                     hipLaunchKernelGGL(ring_read<8>, dim3(grid), dim3(512), 0, 0, ring, ncol, out, 2000);
                 else
                     hipLaunchKernelGGL(ring_read<16>, dim3(grid), dim3(512), 0, 0, ring, ncol, out, 2000);
-                hipEventRecord(e1);
-                hipEventSynchronize(e1);
                 float ms = 0;
-                hipEventElapsedTime(&ms, e0, e1);
+                if (hipEventRecord(e1) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                    hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+                    printf("launch failed\n");
+                    return 1;
+                }
                 printf("rep %d, %2d-B loads, grid %d: %.3f ms, %.0f GB/s\n", rep, w ? 16 : 8, grid, ms,
                        ncol * kSeg * 4.0 / ms / 1e6);
             }
