@@ -1,3 +1,8 @@
+"""Hopf FC conditioning probe (GPU box): the device trajectories of three seeds against the oracle's,
+then both trajectories through the same scipy filtfilt + corrcoef, so the FC difference that
+trajectory-level agreement leaves is separated from the device FC chain's own error (the band
+filter near Nyquist turns 1e-16 input differences into ~1e-7 FC differences; DESIGN §4,
+tests/test_hopf_gpu.py).  Test infrastructure: imports the oracle as the checker."""
 import numpy as np
 from scipy import signal
 import oracle
