@@ -232,6 +232,7 @@ def run_workload(sc, G, S, keys, p, args, dev, dist, steps, warmup):
     for _ in range(steps):
         step()
     flush_welch()  # (an odd step count: the last segment alone, inside the timed region)
+    bt.check()  # waits for the stream; raises if an integrator call failed on the device
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

@@ -12,9 +12,9 @@
  *  - every array argument is DEVICE memory owned by the caller (e.g. a
  *    torch.cuda tensor's data_ptr()), contiguous, batch-major unless stated;
  *  - no allocation inside a call; work is enqueued on `stream` (a hipStream_t,
- *    NULL = default stream) and the call returns without host synchronisation --
- *    except wc_integrate's persistent N > 96 fp32 path, which synchronises `stream`
- *    once per call to read its inter-workgroup hand-off error word (see there);
+ *    NULL = default stream) and the call returns without host synchronisation
+ *    (the one call that waits for the stream is wc_integrate_status, whose
+ *    result is a host value);
  *  - return 0 on success or a negative WC_E* code; wc_last_error() gives a
  *    thread-local message for the last failure on the calling thread;
  *  - reentrant: no global mutable state.
@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define WCSDE_ABI_VERSION 6
+#define WCSDE_ABI_VERSION 7
 
 /* Noise stream (the reference's numba RNG is seeded from os.urandom and never
  * reproducible; the build defines its own): Philox4x32-10 with
@@ -111,10 +111,11 @@ size_t wc_workspace_size(int B, int N, int precision);
  *            be made co-resident (cooperative launch refused: too many blocks, or
  *            the CUs are shared) or WCSDE_PERSISTENT=0, and for fp64: one
  *            GEMM-shaped launch per Euler step (step_kernel), the state in the
- *            workspace between steps.  Both give the same bits.  The persistent
- *            path synchronises `stream` after its launch and returns WC_EHIP if an
- *            inter-workgroup wait timed out (E, I, A are then NaN).  Same noise
- *            stream on every path.
+ *            workspace between steps.  Both give the same bits.  Every wait of
+ *            the persistent path is bounded: one that times out sets the
+ *            workspace's status word and poisons E, I, A with NaN (carried by
+ *            every later call on that state); wc_integrate_status reports it.
+ *            Same noise stream on every path.
  */
 int wc_integrate(const wc_params* p, int precision, int B, int N,
                  const double* sc, const double* G, const double* sigmaE,
@@ -122,6 +123,16 @@ int wc_integrate(const wc_params* p, int precision, int B, int N,
                  int64_t step0, int64_t nsteps, double tau_ip,
                  int64_t rec_every, int64_t rec_ld, void* recE, void* recI, void* recA,
                  void* workspace, size_t ws_bytes, void* stream);
+
+/* Status of the last wc_integrate call on `workspace` (same B, N, precision):
+ * waits for `stream`, then returns WC_EHIP if that call's persistent N > 96
+ * integrator had an inter-workgroup wait time out (its E, I, A are NaN), else 0.
+ * The one wc_integrate-side call that synchronises; call it when the results are
+ * needed anyway (the sweep pipeline: once per batch).  A timed-out call's NaN
+ * state propagates through every later call, so a check at the end of a batch
+ * also covers its earlier calls (the NaN state or this word).  N <= 96: waits
+ * for the stream and returns 0. */
+int wc_integrate_status(const void* workspace, int B, int N, int precision, void* stream);
 
 /* Standard normals the integrator draws at global step `step`: out [B][N]
  * (float or double per precision).  Test hook for the noise stream. */

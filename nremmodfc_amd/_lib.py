@@ -50,6 +50,7 @@ _SIGNATURES = {
     "wc_integrate": (c_int, [ctypes.POINTER(WCParamsC), c_int, c_int, c_int,
                              c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_i64, c_i64, c_dbl, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "wc_integrate_status": (c_int, [c_vp, c_int, c_int, c_int, c_vp]),
     "wc_noise": (c_int, [c_int, c_int, c_int, c_vp, c_i64, c_vp, c_vp]),
     "wc_bold_blocks": (c_i64, [ctypes.POINTER(WCBoldCfgC)]),
     "wc_bold_state_doubles": (c_sz, [ctypes.POINTER(WCBoldCfgC), c_i64]),

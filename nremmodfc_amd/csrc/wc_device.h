@@ -118,7 +118,8 @@ __device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t
 
 // ---------------- fp64 elementary functions for the parity path ----------------
 // Straight-line forms for the inputs this build produces (no special cases, no tables), each
-// within 2 ulp of the correctly rounded value (checked against numpy over the input domains);
+// within 2 ulp of an 80-bit reference over its whole input domain (tests/test_f64m_gpu.py, through
+// the diagnostic build's wc_diag_f64m);
 // ocml's general exp / log / sincospi and the IEEE division sequence took about half of the fp64
 // integrator's VALU.  Coefficients: Taylor series, their truncation below 5e-18 relative.
 namespace f64m {
@@ -159,7 +160,11 @@ __device__ __forceinline__ double log_u24(uint32_t v) {
     const bool hi = f > 1.4142135623730951;
     f = hi ? 0.5 * f : f;
     const double e = (double)(k - 24 + (hi ? 1 : 0));
-    const double s = (f - 1.0) * rcp(f + 1.0);  // f - 1, f + 1 exact
+    // s = (f - 1) / (f + 1) (both exact) to about half an ulp: the product with the reciprocal and
+    // one residual correction (without it the log reached 2.8 ulp where e = 0, v near 2^24)
+    const double num = f - 1.0, den = f + 1.0, rd = rcp(den);
+    double s = num * rd;
+    s = __builtin_fma(__builtin_fma(-s, den, num), rd, s);
     const double s2 = s * s;
     double p = 0.09523809523809523;
     p = __builtin_fma(p, s2, 0.10526315789473684);
@@ -242,7 +247,9 @@ template <> struct Tr<double> {
     __device__ static __forceinline__ acc_t mfma(double a, double b, acc_t c) {
         return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
     }
-    // 1 / (1 + e^(-(x - mu) s)) as 1 / (1 + 2^t), t = (mu - x) s log2(e) (f64m: about 2 ulp)
+    // 1 / (1 + e^(-(x - mu) s)) as 1 / (1 + 2^t), t = (mu - x) s log2(e): exp2 and rcp are within
+    // 2 and 1 ulp, but t is rounded first, so the relative error grows as ~2.1 |t| 2^-53 (tens of
+    // ulp at |t| ~ 40; tests/test_f64m_gpu.py states the measured bound)
     __device__ static __forceinline__ double sig(double x, double mu, double s) {
         return f64m::rcp(1.0 + f64m::exp2((mu - x) * s * 1.4426950408889634));
     }

@@ -37,6 +37,7 @@
 // N > 96: wc_sde_large.hip (fp32: one persistent cooperative launch, the state in registers;
 // fallback and fp64: one GEMM-shaped launch per Euler step)
 size_t wc_large_workspace_size(int B, int N, int precision);
+int wc_large_status(const void* workspace, int B, int N, int precision, hipStream_t st);
 int wc_large_integrate(const wc_params* p, int precision, int B, int N, const double* sc, const double* G,
                        const double* sigmaE, const uint64_t* keys, double* E, double* I, double* A, int64_t step0,
                        int64_t nsteps, double tau_ip, int64_t rec_every, int64_t rec_ld, void* recE, void* recI,
@@ -546,9 +547,9 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                         // pair) and a lane's cells sit at 32-bit element offsets cb + 16 TL(u) + r from it,
                         // so the stores take the saddr form with immediate offsets and no 64-bit cell
                         // address is held across the step loop (eight of them had spilled to scratch)
-                        Real* rE = static_cast<Real*>(a.recE) + (size_t)rec_row * BN;
-                        Real* rI = a.recI ? static_cast<Real*>(a.recI) + (size_t)rec_row * BN : nullptr;
-                        Real* rA = a.recA ? static_cast<Real*>(a.recA) + (size_t)rec_row * BN : nullptr;
+                        Real* recE_row = static_cast<Real*>(a.recE) + (size_t)rec_row * BN;
+                        Real* recI_row = a.recI ? static_cast<Real*>(a.recI) + (size_t)rec_row * BN : nullptr;
+                        Real* recA_row = a.recA ? static_cast<Real*>(a.recA) + (size_t)rec_row * BN : nullptr;
                         const uint32_t cb = (uint32_t)bb * (uint32_t)Nn + (uint32_t)(4 * g + R0);
 #pragma unroll
                         for (int u = 0; u < OT; ++u)
@@ -557,9 +558,9 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                                 const int n = 16 * TL(u) + 4 * g + R0 + r;
                                 if (n < N) {
                                     const uint32_t cc = cb + (uint32_t)(16 * TL(u) + r);
-                                    rE[cc] = E[u][r] * (Real)kEinv;
-                                    if (rI) rI[cc] = I[u][r];
-                                    if (rA) rA[cc] = (Real)A[u][r].get();
+                                    recE_row[cc] = E[u][r] * (Real)kEinv;
+                                    if (recI_row) recI_row[cc] = I[u][r];
+                                    if (recA_row) recA_row[cc] = (Real)A[u][r].get();
                                 }
                             }
                     } else {
@@ -1206,6 +1207,25 @@ int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const 
     return WC_OK;
 }
 
+#ifdef WCSDE_DIAG
+// the fp64 parity path's straight-line elementary functions (wc_device.h, f64m), evaluated alone
+// for tests/test_f64m_gpu.py: 0 exp2(t), 1 rcp(d), 2 log_u24(v), 3 sincospi_v23(v) -> (sin, cos),
+// 4 the fp64 sigmoid Tr<double>::sig(x, mu = 1, s) of (x, s) pairs
+__global__ void f64m_kernel(int fn, int64_t n, const void* __restrict__ in, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double* d = static_cast<const double*>(in);
+    const uint32_t* u = static_cast<const uint32_t*>(in);
+    switch (fn) {
+        case 0: out[i] = f64m::exp2(d[i]); break;
+        case 1: out[i] = f64m::rcp(d[i]); break;
+        case 2: out[i] = f64m::log_u24(u[i]); break;
+        case 3: f64m::sincospi_v23(u[i], out[2 * i], out[2 * i + 1]); break;
+        default: out[i] = Tr<double>::sig(d[2 * i], 1.0, d[2 * i + 1]); break;
+    }
+}
+#endif
+
 }  // namespace
 
 extern "C" {
@@ -1240,6 +1260,19 @@ int wc_integrate(const wc_params* p, int precision, int B, int N, const double* 
     return precision == WC_F64 ? launch_f64(ka, sc, workspace, st) : launch_f32(ka, sc, workspace, st);
 }
 
+int wc_integrate_status(const void* workspace, int B, int N, int precision, void* stream) {
+    wc_clear_err();
+    if (B <= 0 || N <= 0 || (precision != WC_F32 && precision != WC_F64))
+        return wc_set_err(WC_EINVAL, "wc_integrate_status: invalid B/N/precision");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (tiles_for(N) > kMaxTiles) {
+        if (!workspace) return wc_set_err(WC_EWORKSPACE, "wc_integrate_status: NULL workspace");
+        return wc_large_status(workspace, B, N, precision, st);
+    }
+    hipError_t e = hipStreamSynchronize(st);  // N <= 96: nothing can time out; the work is finished
+    return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
+}
+
 #ifdef WCSDE_DIAG
 // declared in csrc/wcsde_diag.h (tools only)
 int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const double* sc, const double* G,
@@ -1263,6 +1296,16 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
     if (tiles_for(N) != 6) return wc_set_err(WC_EUNSUPPORTED, "wc_diag_integrate: needs 81 <= N <= 96");
     if (ws_bytes < wc_workspace_size(B, N, WC_F32)) return wc_set_err(WC_EWORKSPACE, "wc_diag_integrate: workspace");
     return launch_diag(variant, ka, sc, workspace, static_cast<hipStream_t>(stream));
+}
+
+int wc_diag_f64m(int fn, int64_t n, const void* in, double* out, void* stream) {
+    wc_clear_err();
+    if (fn < 0 || fn > 4 || n <= 0 || n > (int64_t(1) << 30) || !in || !out)
+        return wc_set_err(WC_EINVAL, "wc_diag_f64m: bad arguments");
+    hipLaunchKernelGGL(f64m_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       fn, n, in, out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? WC_OK : wc_set_err(WC_EHIP, hipGetErrorString(e));
 }
 #endif  // WCSDE_DIAG
 

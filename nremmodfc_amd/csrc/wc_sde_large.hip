@@ -46,6 +46,7 @@ struct Geo {
 };
 
 size_t al(size_t x) { return (x + 255) & ~size_t(255); }
+size_t status_offset(int B, int N, int precision);
 
 Geo geometry(int B, int N, int precision) {
     Geo g{};
@@ -586,6 +587,8 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
                            reinterpret_cast<double*>(a.ws + g.o_frag));
     }
     const size_t cells = (size_t)g.Bp * g.Np;
+    hipError_t se = hipMemsetAsync(a.ws + status_offset(B, N, sizeof(Real) == 4 ? WC_F32 : WC_F64), 0, 4, st);
+    if (se != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(se));
     hipLaunchKernelGGL(prep_kernel<Real>, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, st, a, G, sigmaE, E,
                        I, A);
     if constexpr (sizeof(Real) == 4) {
@@ -696,9 +699,19 @@ PGeo pgeometry(int B, int N) {
     g.o_scl = o; o += al(2 * sizeof(float));
     g.o_x = o; o += al(2 * (size_t)g.Np * g.Bp * 4);   // two fp16x2 E images
     g.o_cnt = o; o += al((size_t)g.SBp * 64);           // one counter per simulation block, 64 B apart
-    g.o_err = o; o += al(4);
     g.total = o;
+    g.o_err = 0;  // set by status_offset (after both layouts)
     return g;
+}
+
+// The status word of the last N > 96 call on a workspace sits after both layouts (the step and the
+// persistent path reuse the same workspace): each call clears it, a persistent call whose
+// inter-workgroup wait timed out sets it; wc_integrate_status reads it (no host state anywhere).
+size_t status_offset(int B, int N, int precision) {
+    const size_t st = geometry(B, N, precision).total;
+    if (precision != WC_F32) return st;
+    const size_t pe = pgeometry(B, N).total;
+    return st > pe ? st : pe;
 }
 
 struct PArgs {
@@ -1093,6 +1106,7 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
     a.step0 = step0; a.nsteps = nsteps;
     a.ws = static_cast<char*>(workspace);
     a.g = pgeometry(B, N);
+    a.g.o_err = status_offset(B, N, WC_F32);
     // 4 node blocks x 8 simulation blocks per XCD measured 1.5-2% faster than the plain order and
     // than 1, 2 or 8 node blocks per XCD (C5 shard, tools/time_pmap.py); WCSDE_PMAP overrides
     const char* pm = getenv("WCSDE_PMAP");
@@ -1109,7 +1123,8 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
     const int n = g.MT * g.NC * 64;
     hipLaunchKernelGGL(frag_f16_kernel, dim3((n + 255) / 256), dim3(256), 0, st, sc, fg, scl,
                        reinterpret_cast<f16x8*>(a.ws + g.o_frag));
-    hipError_t me = hipMemsetAsync(a.ws + g.o_cnt, 0, g.o_err + al(4) - g.o_cnt, st);  // counters + error word
+    hipError_t me = hipMemsetAsync(a.ws + g.o_cnt, 0, g.total - g.o_cnt, st);  // counters
+    if (me == hipSuccess) me = hipMemsetAsync(a.ws + g.o_err, 0, 4, st);        // this call's status word
     if (me != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(me));
     const dim3 grid((unsigned)(g.SBp * g.NBp)), blk(kPWaves * 64);
     const void* kern = (const void*)persist_kernel<0>;
@@ -1133,18 +1148,9 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
         (void)hipGetLastError();
         return kPersistRetry;
     }
-    // the hand-off's error word: a wait that timed out poisoned the state (NaN); report it
-    // instead of returning plausible partial records (one stream sync per call, >= 2 steps)
-    static thread_local unsigned* herr = nullptr;
-    if (!herr && hipHostMalloc((void**)&herr, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) herr = nullptr;
-    if (!herr) return wc_set_err(WC_EHIP, "wc_integrate: pinned host word for the persistent error check");
-    *herr = 0;
-    if ((e = hipMemcpyAsync(herr, a.ws + g.o_err, sizeof(unsigned), hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess)
-        return wc_set_err(WC_EHIP, hipGetErrorString(e));
-    if (*herr)
-        return wc_set_err(WC_EHIP, "wc_integrate: persistent N > 96 integrator: an inter-workgroup wait timed out "
-                                   "(state poisoned with NaN)");
+    // no host synchronisation: a wait that timed out set the status word and poisoned E, I, a_ie with
+    // NaN (which every later call on this state carries); wc_integrate_status reads the word when the
+    // caller chooses (e.g. at the end of a batch)
     return WC_OK;
 }
 
@@ -1152,10 +1158,19 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
 
 // internal entry points used by wc_sde.hip's dispatcher
 size_t wc_large_workspace_size(int B, int N, int precision) {
-    const size_t st = geometry(B, N, precision).total;
-    if (precision != WC_F32) return st;
-    const size_t pe = pgeometry(B, N).total;  // the persistent path's layout (same workspace, reused)
-    return st > pe ? st : pe;
+    return status_offset(B, N, precision) + al(4);  // both layouts (same workspace, reused) + the status word
+}
+
+int wc_large_status(const void* workspace, int B, int N, int precision, hipStream_t st) {
+    unsigned word = 0;
+    const char* w = static_cast<const char*>(workspace) + status_offset(B, N, precision);
+    hipError_t e = hipMemcpyAsync(&word, w, sizeof(word), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
+    if (word)
+        return wc_set_err(WC_EHIP, "wc_integrate: persistent N > 96 integrator: an inter-workgroup wait timed out "
+                                   "(state poisoned with NaN)");
+    return WC_OK;
 }
 
 int wc_large_integrate(const wc_params* p, int precision, int B, int N, const double* sc, const double* G,

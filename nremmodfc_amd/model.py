@@ -176,6 +176,20 @@ class Batch:
         _lib.check(rc, "wc_integrate")
         self.step += nsteps
 
+    def check(self, stream=None):
+        """Wait for the batch's work and raise if an integrator call failed on the device.
+
+        wc_integrate_status (the one synchronising call of the integrator ABI) reports a timed-out
+        inter-workgroup wait of the last N > 96 call; such a call poisons E, I, a_ie with NaN, which
+        every later call carries, so a NaN state also flags an earlier one.  Called once per batch.
+        """
+        L = _lib.lib()
+        rc = L.wc_integrate_status(_lib.ptr(self.ws), self.B, self.N, _PREC[self.precision],
+                                   _lib.stream_handle(stream))
+        _lib.check(rc, "wc_integrate")
+        if self.N > 96 and bool(torch.isnan(self.E).any()):
+            raise _lib.WCSDEError("wc_integrate: NaN state (an earlier persistent call's wait timed out)")
+
     def state(self):
         return self.E, self.I, self.A
 
@@ -207,4 +221,5 @@ def run_batch(sc, G, sigmaE, keys, schedule: Schedule = None, params: WCParams =
         sl = {n: rec[n][r0:] for n in rec}
         bt.integrate(k, sch.tau_ip[2], R, sl.get("E"), sl.get("I"), sl.get("A"))
         done += k
+    bt.check()
     return rec, bt

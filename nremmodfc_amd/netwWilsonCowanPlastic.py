@@ -160,6 +160,7 @@ def _run(verbose=False):
         bt.integrate(k, 2, ds, rec[0][r0:], rec[1][r0:], rec[2][r0:])
         done += k
         r0 += -(-k // ds)
+    bt.check()
     Y_t = np.zeros((len(time), 3, n))
     m = min(len(time), n_rec)
     for j in range(3):

@@ -134,7 +134,7 @@ def run_sweep(sc, G, sigmaE, keys, empfcs: Dict[str, np.ndarray] = None, schedul
     if welch is not None and next_seg * WELCH_HOP + WELCH_NPERSEG <= T:  # an odd last segment (still in the ring)
         welch.accumulate(ring, ld, chunk_samples, nslots, next_seg * WELCH_HOP)
         next_seg += 1
-    torch.cuda.synchronize(bt.device)  # the phase timings below are of finished work, not queued launches
+    bt.check()  # waits for the stream (the phase timings below are of finished work) and raises on a device failure
     t_sde = time.perf_counter()
     # ---- epilogue ----
     states = tuple(empfcs.keys()) if empfcs else ()

@@ -149,10 +149,18 @@ def append_rows(path, rank, sims, results):
             f.write(format_row(rank, s, r))
 
 
-def collapse(paths, out_csv):
-    """Concatenate per-rank TSV files into the comma-separated table heatmaps.py reads."""
+def collapse(paths, out_csv, sims=None):
+    """Concatenate per-rank TSV files into the comma-separated table heatmaps.py reads.
+
+    With `sims` (the product list) the rows are ordered by (rank, the simulation's index in the
+    list), the order write_gathered uses, whatever order resumed runs appended them in."""
     import pandas as pd
     df = pd.concat([pd.read_csv(p, sep="\t") for p in paths if os.path.exists(p)], ignore_index=True)
+    if sims is not None and len(df):
+        index = {(s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}"): s.index for s in sims}
+        idx = np.array([index.get((int(r.seed), f"{r.delta_G:.4f}", f"{r.delta_sigma:.4f}"), -1)
+                        for r in df.itertuples(index=False)])
+        df = df.iloc[np.lexsort((idx, df["rank"].to_numpy()))].reset_index(drop=True)
     df.to_csv(out_csv, index=False)
     return df
 
@@ -289,7 +297,7 @@ def collapse_sweep(sims, out, tag, world):
     of SLURM-array runs, which have no process group; torchrun runs use write_gathered."""
     paths = [os.path.join(out, "temp", f"{tag}_rank{r}") for r in range(world)]
     tmp = os.path.join(out, f".{tag}.txt.{os.getpid()}")
-    df = collapse(paths, tmp)
+    df = collapse(paths, tmp, sims)
     os.replace(tmp, os.path.join(out, f"{tag}.txt"))
     return _save_rows(sims, out, tag, df)
 
@@ -457,9 +465,11 @@ def main(argv=None):
             f.write(perf + "\n")
         if dist:  # the data path: every rank's whole shard reaches rank 0 in one all-gather over RCCL
             gathered = gather_table(shard_table(rank, mine, todo, rows, path), dist, torch.device(device))
+            # every rank holds the whole gathered table: all ranks check it, so they raise together
+            # (a rank-0-only raise would leave the others blocked in the final barrier)
+            if len(gathered) != len(sims):
+                raise RuntimeError(f"gathered {len(gathered)} rows for {len(sims)} simulations")
             if rank == 0:
-                if len(gathered) != len(sims):
-                    raise RuntimeError(f"gathered {len(gathered)} rows for {len(sims)} simulations")
                 write_gathered(sims, args.out, tag, gathered)
         elif launcher == "slurm":
             if rank_files_complete(sims, args.out, tag, world):  # the last task to finish assembles

@@ -39,7 +39,7 @@ def test_product_library_has_no_diagnostic_entry_points():
 def test_abi_version_and_workspace():
     from nremmodfc_amd import _lib
     L = _lib.lib()
-    assert L.wcsde_abi_version() == 6
+    assert L.wcsde_abi_version() == 7
     # N <= 96: sized for the 3-part 16-bit image (the fp16x2 image and its two scale floats fit inside)
     assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16
     assert L.wc_workspace_size(20000, 90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
@@ -48,9 +48,10 @@ def test_abi_version_and_workspace():
     # (E, I, a_ie pair, G, slope) + 2 fp16x2 E operand images
     Bp, Np = 2560, 1024
     # + per-simulation (G, slope) pairs and the uniformity flag (one 256-B slot)
-    want = (Np // 16) * (Np // 32) * 2 * 64 * 16 + 256 + Bp * Np * (6 * 4 + 2 * 4) + Bp * 8 + 256
+    # + the status word of the last call (one 256-B slot after both layouts)
+    want = (Np // 16) * (Np // 32) * 2 * 64 * 16 + 256 + Bp * Np * (6 * 4 + 2 * 4) + Bp * 8 + 256 + 256
     assert L.wc_workspace_size(2500, 1000, _lib.WC_F32) == want
-    assert L.wc_workspace_size(2500, 1000, _lib.WC_F64) == (Np // 16) * (Np // 4) * 64 * 8 + Bp * Np * 6 * 8
+    assert L.wc_workspace_size(2500, 1000, _lib.WC_F64) == (Np // 16) * (Np // 4) * 64 * 8 + Bp * Np * 6 * 8 + 256
 
 
 def test_invalid_arguments_fail_loudly():

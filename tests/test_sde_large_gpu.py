@@ -110,7 +110,7 @@ def _both_paths(sc, G, S, keys, steps, rec_every=20, rec_ld=0, chunks=None):
                 for n in (chunks or [steps]):
                     b.integrate(n, 2.0, rec_every, rec[done // rec_every:])
                     done += n
-            torch.cuda.synchronize()
+            b.check()  # wc_integrate_status: no wait of the last call timed out (and the state is finite)
             out[flag] = (b.E.clone(), b.I.clone(), b.A.clone(), rec)
         finally:
             os.environ.pop("WCSDE_PERSISTENT", None)
@@ -152,3 +152,25 @@ def test_persistent_maps_ring_and_chunks(cuda):
     p, s = _both_paths(sc, G, S, keys, 200, rec_every=20, chunks=[40, 100, 60])
     for x, y in zip(p, s):
         assert torch.equal(x, y)
+
+
+def test_integrate_status_is_stream_ordered(cuda):
+    """ABI 7: wc_integrate returns without waiting (the persistent path keeps no host word and does
+    not synchronise); wc_integrate_status waits for the stream and reads the last call's status word
+    from the workspace.  A call on a side stream is still running when wc_integrate returns."""
+    from nremmodfc_amd import _lib
+    N, B = 1000, 2500
+    sc = _sc(N, 3)
+    keys = sim_keys(np.arange(B) % 50, np.arange(B) // 50)
+    b = Batch(sc, 0.16, 7.68, keys, precision="f32")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        b.integrate(2000, 2.0, stream=s)  # ~40 ms of persistent work
+        ev = torch.cuda.Event()
+        ev.record(s)
+    assert not ev.query(), "wc_integrate waited for its stream"
+    L = _lib.lib()
+    assert L.wc_integrate_status(_lib.ptr(b.ws), B, N, _lib.WC_F32, _lib.stream_handle(s)) == 0
+    assert ev.query()
+    assert torch.isfinite(b.E).all()

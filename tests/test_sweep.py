@@ -259,6 +259,33 @@ def test_collapse_waits_for_every_rank_file(tmp_path):
     np.testing.assert_allclose(rows[:, 4], np.round(np.arange(7), 4))
 
 
+def test_collapse_orders_rows_like_the_gathered_path(tmp_path):
+    """A resumed run can append a shard's rows out of shard order; the file path sorts by (rank,
+    index), as write_gathered does, so both paths give the same bytes for any append order."""
+    out = str(tmp_path)
+    sims = sweep.homogeneous(1)[:9]
+    os.makedirs(os.path.join(out, "temp"), exist_ok=True)
+    for r in range(2):
+        mine = sweep.shard(sims, r, 2)
+        rows = [{c: s.index + 0.001 * j for j, c in enumerate(sweep.METRIC_COLS)} for s in mine]
+        path = os.path.join(out, "temp", f"o_rank{r}")
+        # the second half first, then the first (a non-prefix resume)
+        h = len(mine) // 2
+        sweep.append_rows(path, r, mine[h:], rows[h:])
+        sweep.append_rows(path, r, mine[:h], rows[:h])
+    sweep.collapse_sweep(sims, out, "o", 2)
+    import pandas as pd
+    df = pd.read_csv(os.path.join(out, "o.txt"))
+    order = [s.index for r in range(2) for s in sweep.shard(sims, r, 2)]
+    np.testing.assert_allclose(df[sweep.METRIC_COLS[0]].to_numpy(), np.array(order, dtype=float), atol=1e-9)
+    table = np.array([[r, s.index, 0, 0] + [s.index + 0.001 * j for j in range(len(sweep.METRIC_COLS))]
+                      for r in range(2) for s in sweep.shard(sims, r, 2)], dtype=float)
+    os.makedirs(os.path.join(out, "g"), exist_ok=True)
+    sweep.write_gathered(sims, os.path.join(out, "g"), "o", table[::-1].copy())
+    with open(os.path.join(out, "g", "o.txt"), "rb") as a, open(os.path.join(out, "o.txt"), "rb") as b:
+        assert a.read() == b.read()
+
+
 def test_slurm_rank_world(monkeypatch):
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setenv("SLURM_ARRAY_TASK_ID", "3")

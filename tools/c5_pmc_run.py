@@ -13,7 +13,18 @@ from nremmodfc_amd import datasets  # noqa: E402
 from nremmodfc_amd.model import Batch, driver_params  # noqa: E402
 
 
+def _dump_maps():
+    """/proc/self/maps at Python exit (before the C-level exit handlers), so that the frames of a
+    fault during process teardown can be mapped to library + offset."""
+    out = os.environ.get("C5_MAPS_OUT")
+    if out:
+        with open("/proc/self/maps") as f, open(out, "w") as g:
+            g.write(f.read())
+
+
 def main():
+    import atexit
+    atexit.register(_dump_maps)
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 400
     sc = datasets.synthetic_sc(1000)
     G, S, keys = bench.sweep_batch(0)

@@ -1,7 +1,8 @@
 #!/bin/bash
 # ONE rocprofv3 --pmc pass over tools/c5_pmc_run.py (the C5 persistent integrator, one 400-step
-# dispatch), per gpurun call: rocprofv3 writes its CSV and then segfaults in process teardown after
-# the cooperative launch (exit 139 after "tool finalization"), and a call stops at a segfault.
+# dispatch), per gpurun call.  (Round 4's passes segfaulted in process teardown after "tool
+# finalization"; tools/c5_pmc_run.py writes /proc/self/maps at exit to $OUT/<pass>.maps so that the
+# frames of such a fault map to library + offset.)
 #   PASS = fetch | write | sqa | sqb | tcc (L2 hits and misses)  -> gpurun_out/prof_c5/<pass>/ ; then tools/profile_c5_summary.py
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -16,6 +17,7 @@ case $P in
   sqb) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU GRBM_GUI_ACTIVE" ;;
   *) echo "unknown pass $P"; exit 2 ;;
 esac
+export C5_MAPS_OUT=$OUT/$P.maps
 timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $OUT/$P -o p -- python3 tools/c5_pmc_run.py 400 > $OUT/$P.log 2>&1
 rc=$?
 grep -q "persist_kernel" $OUT/$P/p_counter_collection.csv && echo "pass $P: counters written (rocprofv3 rc=$rc)"
