@@ -68,6 +68,15 @@ def sweep_batch(rank, n_seeds=50, nG=20, nS=20):
     return G, S, keys
 
 
+def loaded_lib_sha256():
+    """sha256 of the libwcsde.so this process loads (nremmodfc_amd/_build.py LIB_LOAD): the stamp a
+    profiles/pmc_*.json must carry for its counters to be attached to the bench line."""
+    import hashlib
+    from nremmodfc_amd import _build
+    with open(_build.LIB_LOAD, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 CPU_SHARE = 16  # host cores one GPU's job may use on the GPU box (its OMP_NUM_THREADS / MAX_JOBS)
 
 
@@ -79,7 +88,7 @@ def _cores():
     return avail, max(1, min(avail, CPU_SHARE))
 
 
-def cpu_baseline_numpy(steps=150_000):
+def cpu_baseline_numpy(steps=150_000, nodes=90):
     """The reference's own hot loop as NumPy executes it (oracle/numpy_run.py: wc:72-137 operation
     for operation, bit-identical to the reference's run() under the same normals), one
     single-threaded process per core as the reference's SLURM array runs it,
@@ -89,7 +98,7 @@ def cpu_baseline_numpy(steps=150_000):
     avail, ncores = _cores()
     env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
     t0 = time.perf_counter()
-    procs = [subprocess.Popen([sys.executable, "-m", "oracle.numpy_run", str(steps), str(i)], cwd=ROOT, env=env,
+    procs = [subprocess.Popen([sys.executable, "-m", "oracle.numpy_run", str(steps), str(i), str(nodes)], cwd=ROOT, env=env,
                               stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True) for i in range(ncores)]
     secs = []
     for pr in procs:
@@ -98,12 +107,13 @@ def cpu_baseline_numpy(steps=150_000):
             raise RuntimeError("cpu_baseline_numpy: a worker failed")
         secs.append(float(out.strip().splitlines()[-1]))
     wall = time.perf_counter() - t0
-    per_core = [90 * steps / s for s in secs]
-    value = 90 * steps * ncores / max(secs)  # every worker's node-steps over the slowest worker's loop time
+    per_core = [nodes * steps / s for s in secs]
+    value = nodes * steps * ncores / max(secs)  # every worker's node-steps over the slowest worker's loop time
+    net = "N=90" if nodes == 90 else f"N={nodes} (datasets.synthetic_sc: np.dot(CM, E) a BLAS gemv per step)"
     return {"value": value, "unit": "node-timesteps/sec", "cores": ncores, "kind": "port",
             "cores_available": avail, "cores_cap": CPU_SHARE,
             "per_core": {"mean": float(np.mean(per_core)), "min": float(min(per_core))},
-            "sample": f"{ncores} processes x 1 sim x {steps} Euler steps of the C3 cell (0.16, 7.68), N=90: the "
+            "sample": f"{ncores} processes x 1 sim x {steps} Euler steps of the C3 cell (0.16, 7.68), {net}: the "
                       f"reference's NumPy loop (oracle/numpy_run.py, bit-identical to netwWilsonCowanPlastic.py's "
                       f"run() under replayed noise), numpy's normal draws, 1 BLAS thread each; {wall:.1f} s wall",
             "note": "cores capped at one GPU's host share on the box (CPU_SHARE)"}
@@ -118,7 +128,7 @@ def cpu_baseline_compiled(sc, seconds=8.0, steps=2000):
     p = driver_params()
     B = 2 * ncores
     ob = oracle.OracleBatch(sc, G[:B], S[:B], keys[:B], p)
-    ob.integrate(200, 2.0, 20, nthreads=ncores)  # warm
+    ob.integrate(min(200, steps), 2.0, 20, nthreads=ncores)  # warm
     total, t0, n = 0, time.perf_counter(), 0
     while True:
         ob.integrate(steps, 2.0, 20, nthreads=ncores)
@@ -129,23 +139,38 @@ def cpu_baseline_compiled(sc, seconds=8.0, steps=2000):
     ns = B * sc.shape[0] * steps * n
     return {"value": ns / total, "unit": "node-timesteps/sec", "cores": ncores, "kind": "port",
             "cores_available": avail, "cores_cap": CPU_SHARE,
-            "sample": f"{B} sims x {steps * n} Euler steps of the C3 grid (tau_ip=2, E recorded every "
-                      f"20 steps), oracle/wc_oracle.c fp64 (the compiled loop numba gives the reference), "
-                      f"OpenMP over simulations, {ncores} threads, {total:.1f} s",
+            "per_core": ns / total / ncores,
+            "sample": f"{B} sims x {steps * n} Euler steps of the C3 grid on N={sc.shape[0]} (tau_ip=2, E recorded "
+                      f"every 20 steps), oracle/wc_oracle.c fp64 (the compiled loop numba gives the reference; "
+                      f"its CM.E is a scalar dot loop), OpenMP over simulations, {ncores} threads, {total:.1f} s",
             "note": "cores capped at one GPU's host share on the box (CPU_SHARE = 16 of the affinity mask's "
                     "cores_available); profiles/r04_cpu_scaling.log has the per-core rate at 1..16 cores"}
 
 
 def cpu_baseline(sc, seconds=8.0, steps=2000):
-    """The reported baseline is the compiled port (oracle/wc_oracle.c): the reference decorates run()
-    and wilsonCowan with numba's @njit (netwWilsonCowanPlastic.py:77,86) and cannot be imported
-    without numba, so as shipped its loop always runs compiled.  The interpreted NumPy restatement
-    (the same loop without the JIT) is reported beside it as `numpy_interpreted`; `seconds` sizes
-    both (about 2 x seconds of CPU work in total)."""
-    out = cpu_baseline_compiled(sc, seconds, steps)
-    out["numpy_interpreted"] = cpu_baseline_numpy(steps=max(2000, int(seconds * 20_000)))
-    out["numpy_interpreted"]["kind"] = "interpreted"
-    return out
+    """N = 90: the reported baseline is the compiled port (oracle/wc_oracle.c): the reference
+    decorates run() and wilsonCowan with numba's @njit (netwWilsonCowanPlastic.py:77,86) and cannot
+    be imported without numba, so as shipped its loop always runs compiled.  The interpreted NumPy
+    restatement (the same loop without the JIT) is reported beside it as `numpy_interpreted`.
+
+    N = 1000 (C5): the step is dominated by np.dot(CM, E) (wc:81), a 1e6-MAC gemv, which numba and
+    NumPy both hand to BLAS; the NumPy loop then runs at the compiled rate and the C port's scalar
+    dot loop is slower.  Both legs run; the faster is `value` (the other beside it), so the GPU is
+    compared against the better of the two CPU forms.  `seconds` sizes each leg."""
+    N = sc.shape[0]
+    if N == 90:
+        out = cpu_baseline_compiled(sc, seconds, steps)
+        out["numpy_interpreted"] = cpu_baseline_numpy(steps=max(2000, int(seconds * 20_000)))
+        out["numpy_interpreted"]["kind"] = "interpreted"
+        return out
+    comp = cpu_baseline_compiled(sc, seconds, steps=max(20, int(steps * (90 / N) ** 2)))
+    nump = cpu_baseline_numpy(steps=max(200, int(seconds * 2_000_000 / N)), nodes=N)
+    best, other, oname = (nump, comp, "compiled_port") if nump["value"] >= comp["value"] else (comp, nump, "numpy_interpreted")
+    best = dict(best)
+    best[oname] = other
+    best["note"] = (f"N={N}: the faster of the reference's NumPy loop (BLAS gemv for np.dot(CM, E), wc:81) and the "
+                    f"compiled C port; " + best.get("note", ""))
+    return best
 
 
 def run_workload(sc, G, S, keys, p, args, dev, dist, steps, warmup):
@@ -334,26 +359,31 @@ def main():
     per_launch_ns = B * N * EULER
     t_launch = kern["sde"] * 1e-3
     pmc_d = {}
-    pmc = os.path.join(ROOT, "profiles", "pmc_sde.json" if args.config == "c3" else "pmc_sde_c5.json")
-    if os.path.exists(pmc):
+    pmc_refused = []
+    stamp = loaded_lib_sha256()
+
+    def stamped(path):
+        """profiles/pmc_*.json, only if its counters were taken on the library this process runs."""
         try:
-            d = json.load(open(pmc))
-            if d.get("B") == B and d.get("N") == N and d.get("euler_steps") == EULER and \
-                    d.get("precision") == args.precision and \
-                    (N <= 96 or ("persist" in d.get("kernel", "")) == (os.environ.get("WCSDE_PERSISTENT") != "0")):
-                pmc_d = d
+            d = json.load(open(path)) if os.path.exists(path) else {}
         except (ValueError, OSError):
-            pmc_d = {}
+            return {}
+        if d and d.get("lib_sha256") != stamp:
+            pmc_refused.append({"file": os.path.relpath(path, ROOT), "stamp": d.get("lib_sha256"), "loaded": stamp})
+            return {}
+        return d
+    pmc = os.path.join(ROOT, "profiles", "pmc_sde.json" if args.config == "c3" else "pmc_sde_c5.json")
+    d = stamped(pmc)
+    if d.get("B") == B and d.get("N") == N and d.get("euler_steps") == EULER and \
+            d.get("precision") == args.precision and \
+            (N <= 96 or ("persist" in d.get("kernel", "")) == (os.environ.get("WCSDE_PERSISTENT") != "0")):
+        pmc_d = d
     traffic = pmc_d.get("hbm_bytes_per_launch")
     util = {k: pmc_d[k] for k in ("valu_insts_per_wave_step", "mfma_insts_per_wave_step", "mfma_busy_frac")
             if k in pmc_d}
     if N > 96 and pmc_d:
         # the persistent kernel's SQ counters come from their own PMC passes (tools/profile_c5_pass.sh sqa / sqb, tools/profile_c5_summary.py)
-        sqf = os.path.join(ROOT, "profiles", "pmc_c5_sq.json")
-        try:
-            q = json.load(open(sqf)) if os.path.exists(sqf) else {}
-        except (ValueError, OSError):
-            q = {}
+        q = stamped(os.path.join(ROOT, "profiles", "pmc_c5_sq.json"))
         if q.get("kernel") == pmc_d.get("kernel"):
             util.update({k: q[k] for k in ("mfma_busy_frac", "valu_issue_busy_frac", "salu_per_wave_step") if k in q})
             util.update({f"{k.lower()}_per_wave_step": v for k, v in q.get("per_wave_step", {}).items()})
@@ -417,6 +447,9 @@ def main():
                         "state streaming, which this kernel no longer moves"}
     roof["kernel_ms_per_launch"] = kern["sde"]
     roof["pmc"] = util or None
+    roof["pmc_lib_sha256"] = stamp if pmc_d else None
+    if pmc_refused:  # counters of another build are not attached (they would describe other code)
+        roof["pmc_refused"] = pmc_refused
     roof["issued_mfma"] = issued if N <= 96 else None
     out = {
         "metric": "node-timesteps/sec (90-node WC, (G,sigma)x50-seed sweep) at 1/2/4/8 GPUs"
@@ -448,7 +481,7 @@ def main():
         "kernel_ms": kern,
         "weak_scaling": weak,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c3":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(sc, seconds=args.cpu_seconds)
     elif rank == 0:
         out["cpu_baseline"] = None

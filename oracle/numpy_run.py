@@ -56,9 +56,11 @@ def run(p, CM, G, sigmaE, n1, n2, n3, rec_every=20, normal=np.random.normal, mu=
     return Y_t
 
 
-def timed_sample(steps, seed=0):
+def timed_sample(steps, seed=0, nodes=90):
     """One simulation of the C3 cell (0.16, 7.68) for `steps` recorded-phase steps on the
-    90-node connectome, numpy's own normal draws (the reference's RNG call): -> seconds."""
+    90-node connectome (nodes = 1000: the C5 synthetic connectome, datasets.synthetic_sc, where
+    np.dot(CM, E) of wc:81 is a BLAS gemv of 1e6 multiply-adds per step), numpy's own normal
+    draws (the reference's RNG call): -> seconds."""
     import time
     import types
 
@@ -67,13 +69,13 @@ def timed_sample(steps, seed=0):
     # plain namespace so a worker imports numpy only (nremmodfc_amd.model would import torch)
     p = types.SimpleNamespace(a_ee=3.5, a_ie_0=2.5, a_ei=3.75, a_ii=0, tauE=0.010, tauI=0.020, P=0.4, rhoE=0.18,
                               rE=0.5, rI=0.5, sigmaI=4, sqdtD=0.002 / np.sqrt(0.0001), dtSim=0.0001, E0=0.1, I0=0.1)
-    sc = datasets.load_sc()
+    sc = datasets.load_sc() if nodes == 90 else datasets.synthetic_sc(nodes)
     np.random.seed(seed)
     t0 = time.perf_counter()
     run(p, sc, 0.16, 7.68, 0, 0, steps, 20)
     return time.perf_counter() - t0
 
 
-if __name__ == "__main__":  # worker of bench.py's cpu_baseline: python -m oracle.numpy_run STEPS SEED
+if __name__ == "__main__":  # worker of bench.py's cpu_baseline: python -m oracle.numpy_run STEPS SEED [NODES]
     import sys
-    print(timed_sample(int(sys.argv[1]), int(sys.argv[2])), flush=True)
+    print(timed_sample(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]) if len(sys.argv) > 3 else 90), flush=True)

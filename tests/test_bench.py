@@ -29,6 +29,28 @@ def test_cpu_baseline_leg():
     assert npy["cores"] == cb["cores"]
 
 
+def test_cpu_baseline_leg_n1000():
+    """C5's CPU baseline: the reference's NumPy loop at N = 1000 (np.dot(CM, E) a
+    BLAS gemv, wc:81) and the compiled C port, the faster as the value, the other beside it."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from nremmodfc_amd import datasets
+    cb = bench.cpu_baseline(datasets.synthetic_sc(1000), seconds=0.2, steps=200)
+    other = cb.get("compiled_port") or cb.get("numpy_interpreted")
+    assert cb["value"] >= other["value"] > 0 and "N=1000" in cb["sample"] and "N=1000" in other["sample"]
+    assert cb["cores"] == other["cores"] == min(cb["cores_available"], cb["cores_cap"])
+
+
+def test_pmc_stamp_is_the_loaded_library():
+    sys.path.insert(0, ROOT)
+    import hashlib
+
+    import bench
+    from nremmodfc_amd import _build
+    _build.build()
+    assert bench.loaded_lib_sha256() == hashlib.sha256(open(_build.LIB_LOAD, "rb").read()).hexdigest()
+
+
 @pytest.mark.gpu
 def test_bench_json_contract(cuda):
     out = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--cpu-seconds", "1"],
@@ -57,7 +79,7 @@ def test_bench_json_contract(cuda):
 @pytest.mark.gpu
 def test_bench_c5_line_priced_on_mfma(cuda):
     out = subprocess.run([sys.executable, "bench.py", "--config", "c5", "--steps", "1", "--warmup", "0",
-                          "--sde-only"], cwd=ROOT, capture_output=True, text=True, timeout=100)
+                          "--sde-only", "--cpu-seconds", "1"], cwd=ROOT, capture_output=True, text=True, timeout=150)
     assert out.returncode == 0, out.stderr[-2000:]
     d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
     r = d["roofline"]
@@ -66,3 +88,7 @@ def test_bench_c5_line_priced_on_mfma(cuda):
     o = r["operand_stream"]
     assert r["binding"] == "operand_stream" and abs(o["frac"] - o["GBps"] / o["peak_GBps"]) < 1e-12
     assert d["config"]["nodes"] == 1000 and d["config"]["sims_per_gpu"] == 2500
+    # the CPU baseline at N = 1000 in the same run (north_star)
+    assert d["cpu_baseline"]["value"] > 0 and "N=1000" in d["cpu_baseline"]["sample"]
+    # counters are attached only when taken on the library this run loaded
+    assert r["pmc"] is None or r["pmc_lib_sha256"] is not None

@@ -11,15 +11,18 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
 ARGS="--steps ${PSTEPS:-4} --warmup 1 --no-cpu-baseline"
+STAMP=$(sha256sum nremmodfc_amd/libwcsde.so | cut -d' ' -f1)  # the library every pass below runs
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o bench -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o p -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o p -- python3 bench.py $ARGS > $OUT/write.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VALU_TRANS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o p -- python3 bench.py $ARGS > $OUT/sq.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq2 -o p -- python3 bench.py $ARGS > $OUT/sq2.log 2>&1
+for d in $OUT/fetch $OUT/write $OUT/sq $OUT/sq2; do mkdir -p $d && echo $STAMP > $d/lib.sha256; done
 python3 - <<'PY'
 import json, sys
 sys.path.insert(0, "tools")
-from pmc_summary import summary
+from pmc_summary import lib_stamp, summary
+stamp = lib_stamp("gpurun_out/prof/fetch", "gpurun_out/prof/write", "gpurun_out/prof/sq", "gpurun_out/prof/sq2")
 f = summary("gpurun_out/prof/fetch", "wc_sde_kernel")
 w = summary("gpurun_out/prof/write", "wc_sde_kernel")
 q = summary("gpurun_out/prof/sq", "wc_sde_kernel")
@@ -32,7 +35,7 @@ B, N, STEPS = 20000, 90, 20000
 node_steps = B * N * STEPS
 wave_steps = (B // 16) * 3 * STEPS  # 16 simulations x 3 waves (2 node tiles each) per group
 simds = 256 * 4
-d = {"kernel": kf, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
+d = {"kernel": kf, "lib_sha256": stamp, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
      "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
      "hbm_bytes_per_launch": fetch + write, "dispatches": vf["dispatches"],
      "algorithmic_bytes_per_launch": B * N * (STEPS // 20 * 4 + 2 * 3 * 8 + 2 * 8),
@@ -52,7 +55,7 @@ q2 = summary("gpurun_out/prof/sq2", "wc_sde_kernel")
 d["wave_cycle_split"] = {k: v2[k] / v2["SQ_WAVE_CYCLES"] for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")}
 json.dump(d, open("profiles/pmc_sde.json", "w"), indent=1)
 # the two signal kernels of the bench step: instruction counts per unit of work, issue and wait split
-sig = {"note": "rocprofv3 --pmc passes of the same bench run (tools/profile_bench.sh), averaged per dispatch. "
+sig = {"lib_sha256": stamp, "note": "rocprofv3 --pmc passes of the same bench run (tools/profile_bench.sh), averaged per dispatch. "
                "Busy fractions: 4 x SQ_ACTIVE_INST_* quad-cycles / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); "
                "wave_cycle_split: SQ_WAIT_ANY (parked on s_waitcnt/barrier), SQ_WAIT_INST_ANY (issue stall), "
                "SQ_ACTIVE_INST_ANY (issuing), fractions of SQ_WAVE_CYCLES."}

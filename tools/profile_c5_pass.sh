@@ -18,6 +18,7 @@ case $P in
   *) echo "unknown pass $P"; exit 2 ;;
 esac
 export C5_MAPS_OUT=$OUT/$P.maps
+mkdir -p $OUT/$P && sha256sum nremmodfc_amd/libwcsde.so | cut -d' ' -f1 > $OUT/$P/lib.sha256  # the library this pass runs
 timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $OUT/$P -o p -- python3 tools/c5_pmc_run.py 400 > $OUT/$P.log 2>&1
 rc=$?
 grep -q "persist_kernel" $OUT/$P/p_counter_collection.csv && echo "pass $P: counters written (rocprofv3 rc=$rc)"

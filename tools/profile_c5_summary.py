@@ -7,13 +7,15 @@ def hbm():
     import json, os, sys
     sys.path.insert(0, "tools")
     from pmc_summary import summary
+    from pmc_summary import lib_stamp
+    stamp = lib_stamp("gpurun_out/prof_c5/fetch", "gpurun_out/prof_c5/write")
     (kf, vf), = summary("gpurun_out/prof_c5/fetch", "persist_kernel").items()
     (kw, vw), = summary("gpurun_out/prof_c5/write", "persist_kernel").items()
     B, N, STEPS = 2500, 1000, 20000
     RUN = int(os.environ.get("C5STEPS", "400"))  # one persist_kernel launch integrates RUN steps
     fetch = 2 * vf["FETCH_SIZE"] * 1024.0 / RUN
     write = vw["WRITE_SIZE"] * 1024.0 / RUN
-    d = {"kernel": kf, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
+    d = {"kernel": kf, "lib_sha256": stamp, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
          "fetch_bytes_per_step": fetch, "write_bytes_per_step": write,
          "fetch_bytes_per_launch": fetch * STEPS, "write_bytes_per_launch": write * STEPS,
          "hbm_bytes_per_launch": (fetch + write) * STEPS, "dispatches": vf["dispatches"],
@@ -31,11 +33,13 @@ def sq():
     import json, sys
     sys.path.insert(0, "tools")
     from pmc_summary import summary
+    from pmc_summary import lib_stamp
+    stamp = lib_stamp("gpurun_out/prof_c5/sqa", "gpurun_out/prof_c5/sqb")
     (ka, a), = summary("gpurun_out/prof_c5/sqa", "persist_kernel").items()
     (_, b), = summary("gpurun_out/prof_c5/sqb", "persist_kernel").items()
     STEPS, WAVES = 400, 256 * 8
     act = a["GRBM_GUI_ACTIVE"] / 8 * 1024
-    d = {"kernel": ka, "steps": STEPS, "waves": WAVES,
+    d = {"kernel": ka, "lib_sha256": stamp, "steps": STEPS, "waves": WAVES,
          "per_wave_step": {k: a[k] / (WAVES * STEPS) for k in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD")},
          "salu_per_wave_step": b["SQ_INSTS_SALU"] / (WAVES * STEPS),
          "mfma_busy_frac": a["SQ_VALU_MFMA_BUSY_CYCLES"] / act,
@@ -53,10 +57,12 @@ def tcc():
     import json, sys
     sys.path.insert(0, "tools")
     from pmc_summary import summary
+    from pmc_summary import lib_stamp
+    stamp = lib_stamp("gpurun_out/prof_c5/tcc")
     (k, t), = summary("gpurun_out/prof_c5/tcc", "persist_kernel").items()
     STEPS = 400
     req = t["TCC_HIT_sum"] + t["TCC_MISS_sum"]
-    d = {"kernel": k, "steps": STEPS,
+    d = {"kernel": k, "lib_sha256": stamp, "steps": STEPS,
          "tcc_requests_per_step": req / STEPS, "tcc_hits_per_step": t["TCC_HIT_sum"] / STEPS,
          "tcc_misses_per_step": t["TCC_MISS_sum"] / STEPS, "l2_hit_rate": t["TCC_HIT_sum"] / req,
          "ea_read_requests_per_step": t["TCC_EA0_RDREQ_sum"] / STEPS,
