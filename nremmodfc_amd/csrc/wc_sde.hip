@@ -1094,6 +1094,9 @@ int launch_f32(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
 // fp64 parity path: one wave per node tile (NW = NT; E exchanged through LDS), so the
 // latency-bound step of a small batch is spread over NT waves; the per-tile MFMA order is
 // the one-wave kernel's, so the results are the same bits for any NW
+#ifndef WC_F64_SG
+#define WC_F64_SG 2
+#endif
 int launch_f64(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     switch (tiles_for(ka.N)) {
         case 1: return launch_v<double, 1, 1, kVarF64>(ka, sc, ws, st);
@@ -1101,7 +1104,9 @@ int launch_f64(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
         case 3: return launch_v<double, 3, 3, kVarF64>(ka, sc, ws, st);
         case 4: return launch_v<double, 4, 4, kVarF64>(ka, sc, ws, st);
         case 5: return launch_v<double, 5, 5, kVarF64>(ka, sc, ws, st);
-        case 6: return launch_v<double, 6, 6, kVarF64>(ka, sc, ws, st);
+        // N 81..96: WC_F64_SG groups of 16 simulations per workgroup share one LDS copy of the fp64
+        // connectome image (73.7 KB): 2 groups (12 waves) per CU instead of one
+        case 6: return launch_v<double, 6, 6, kVarF64, 1, WC_F64_SG>(ka, sc, ws, st);
         default: return wc_set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
     }
 }

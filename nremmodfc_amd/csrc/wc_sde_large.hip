@@ -265,11 +265,13 @@ __device__ __forceinline__ void st_state(T* p, T v) {
 
 // wc:80-83 for one (node, simulation) cell on the fp32 product path: the folded-constant form of
 // wc_sde.hip's fast path (x' = xE - mu, log2-based sigmoids, the noise scale with sqrt(2 ln 2)
-// folded in for the raw Box-Muller normal, a_ie read as its high word), with every fusion
-// explicit (contraction off inside).  step_kernel and persist_kernel both call this, so the two
-// N > 96 paths give the same bits whatever the surrounding code lets the compiler fuse.
+// folded in for the raw Box-Muller normal, a_ie read as its high word, the a_ie increment as
+// in (E dtA - rhoE dtA)), with every fusion explicit (contraction off inside).  step_kernel calls
+// the scalar form, persist_kernel the packed pair form (v_pk_fma/mul/add_f32 round each
+// component exactly like the scalar instruction), so the two N > 96 paths give the same bits
+// whatever the surrounding code lets the compiler fuse.
 struct CellConsts {
-    float a_ee, Pm, rhoE, rE, rI, cIe, cIi, cI0, knoise, dtE, dtI, dtA;
+    float a_ee, Pm, rhoE, rE, rI, cIe, cIi, cI0, knoise, dtE, dtI, dtA, cA;
 };
 #pragma clang fp contract(off)
 __device__ __forceinline__ void cell_update_f32(const CellConsts& k, float& e, float& in, AccA<true>& A, float cpl,
@@ -284,8 +286,40 @@ __device__ __forceinline__ void cell_update_f32(const CellConsts& k, float& e, f
     const float SI = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(__builtin_fmaf(e0, k.cIe, __builtin_fmaf(in0, k.cIi, k.cI0))));
     e = pad ? 0.f : __builtin_fmaf(k.dtE, __builtin_fmaf(__builtin_fmaf(-k.rE, e0, 1.0f), SE, -e0), e0);
     in = __builtin_fmaf(k.dtI, __builtin_fmaf(__builtin_fmaf(-k.rI, in0, 1.0f), SI, -in0), in0);
-    const float tA = in0 * k.dtA;
-    A.add(__builtin_fmaf(e0, tA, -k.rhoE * tA));
+    A.add(in0 * __builtin_fmaf(e0, k.dtA, k.cA));
+}
+
+// the same update for two cells of one simulation (nodes r, r + 1: one G and slope), packed
+struct CellConsts2 {
+    f2v a_ee, Pm, cIe, cIi, cI0, knoise, dtE, dtI, dtA, cA, nrE, nrI;
+};
+__device__ __forceinline__ CellConsts2 cell_consts2(const CellConsts& k) {
+    auto b = [](float v) { return f2v{v, v}; };
+    return CellConsts2{b(k.a_ee), b(k.Pm), b(k.cIe), b(k.cIi), b(k.cI0), b(k.knoise), b(k.dtE), b(k.dtI), b(k.dtA),
+                       b(k.cA), b(-k.rE), b(-k.rI)};
+}
+__device__ __forceinline__ void cell_pair_f32(const CellConsts2& k, f2v& e, f2v& in, f2v& ahi, f2v& alo, f2v cpl,
+                                              f2v G, f2v sl, f2v z, bool pad0, bool pad1) {
+    const f2v e0 = e, in0 = in, one = {1.0f, 1.0f};
+    f2v x = __builtin_elementwise_fma(k.a_ee, e0, k.Pm);
+    x = __builtin_elementwise_fma(-ahi, in0, x);
+    x = __builtin_elementwise_fma(G, cpl, x);
+    x = __builtin_elementwise_fma(k.knoise, z, x);
+    const f2v te = x * sl;
+    const f2v de = one + f2v{__builtin_amdgcn_exp2f(-te.x), __builtin_amdgcn_exp2f(-te.y)};
+    const f2v SE = {__builtin_amdgcn_rcpf(de.x), __builtin_amdgcn_rcpf(de.y)};
+    const f2v ti = __builtin_elementwise_fma(e0, k.cIe, __builtin_elementwise_fma(in0, k.cIi, k.cI0));
+    const f2v di = one + f2v{__builtin_amdgcn_exp2f(ti.x), __builtin_amdgcn_exp2f(ti.y)};
+    const f2v SI = {__builtin_amdgcn_rcpf(di.x), __builtin_amdgcn_rcpf(di.y)};
+    const f2v inc = in0 * __builtin_elementwise_fma(e0, k.dtA, k.cA);
+    const f2v t = inc + alo;  // Kahan-Babuska, as AccA<true>::add
+    const f2v s = ahi + t;
+    alo = t - (s - ahi);
+    ahi = s;
+    e = __builtin_elementwise_fma(k.dtE, __builtin_elementwise_fma(__builtin_elementwise_fma(k.nrE, e0, one), SE, -e0), e0);
+    if (pad0) e.x = 0.f;
+    if (pad1) e.y = 0.f;
+    in = __builtin_elementwise_fma(k.dtI, __builtin_elementwise_fma(__builtin_elementwise_fma(k.nrI, in0, one), SI, -in0), in0);
 }
 #pragma clang fp contract(on)
 
@@ -295,7 +329,8 @@ __host__ __device__ inline CellConsts cell_consts(double a_ee, double a_ei, doub
     const double l2e = 1.4426950408889634;
     return CellConsts{(float)a_ee, (float)(P - mu), (float)rhoE, (float)rE, (float)rI, (float)(-a_ei * sigmaI * l2e),
                       (float)(a_ii * sigmaI * l2e), (float)(mu * sigmaI * l2e), (float)(sqdtD * (double)kSqrt2Ln2),
-                      (float)(dtSim / tauE), (float)(dtSim / tauI), (float)(dtSim / tau_ip)};
+                      (float)(dtSim / tauE), (float)(dtSim / tauI), (float)(dtSim / tau_ip),
+                      (float)(-rhoE * dtSim / tau_ip)};
 }
 
 // one Euler step of every simulation; rec_row >= 0: record the state before the update
@@ -364,12 +399,16 @@ __global__ void __launch_bounds__(256) step_kernel(const LArgs a, int s, int rec
             boff[i] = (pb * 4 + gb) * 64;
         }
         const size_t bstep = (size_t)SB * 256;
+        // K chunks in cyclic order from chunk 4 (mb / 2): the persistent kernel's order for these rows
+        // (its 128-node block's own four chunks first), so both paths accumulate identically
+        const int kc0 = 4 * (mb >> 1);
         auto issue = [&](int c, int st) {
+            const int cc = c + kc0 < g.NC ? c + kc0 : c + kc0 - g.NC;
 #pragma unroll
             for (int i = 0; i < kU; ++i) {
-                __builtin_amdgcn_global_load_lds(asrc[i] + (size_t)c * kParts * 64, (lds_vptr)(&lds[st][0][aoff[i]]), 16,
+                __builtin_amdgcn_global_load_lds(asrc[i] + (size_t)cc * kParts * 64, (lds_vptr)(&lds[st][0][aoff[i]]), 16,
                                                  0, 0);
-                __builtin_amdgcn_global_load_lds(bsrc[i] + (size_t)c * bstep, (lds_vptr)(&lds[st][1][boff[i]]), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds(bsrc[i] + (size_t)cc * bstep, (lds_vptr)(&lds[st][1][boff[i]]), 16, 0, 0);
             }
         };
         const int ua = (w & 1) * 2, ub = (w >> 1) * 2;  // this wave's tiles within the workgroup slab
@@ -612,44 +651,44 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
 
 
 // ============================================================================================
-// Persistent fp32 integrator (round 2): the state stays in registers for the whole call.
+// Persistent fp32 integrator (round 5 layout): the state stays in registers for the whole call.
 //
-// One workgroup (8 waves) owns a tile of 128 nodes x 80 simulations for ALL nsteps steps:
-// wave w holds node tile w (16 nodes) of the five 16-simulation tiles, i.e. 20 (node, sim)
-// cells per lane -- E, I, the a_ie pair, G and the slope in VGPRs.  Each step it streams the
-// connectome rows of its 128 nodes (read-only: LDS-DMA, as in step_kernel) and the whole E
-// image of its 80 simulations, which the 8 node-block workgroups of the simulation block
-// publish every step (every node's E feeds every node's coupling).  The hand-off follows
-// MI355X_MICROARCH.md's fence-free form (its "Valid forms" consumer conditions (1)-(4) with
-// row 1 of the sc1 hand-off table, whose store and load cells admit 4-, 8- or 16-B accesses;
-// DESIGN.md 3.1b quotes them): the E image is stored write-through (16-B sc1 buffer stores
-// under WC_PIMG16, the default; 8-B otherwise) and every load of it is a 16-B sc1 buffer load to
-// registers; every storing wave drains vmcnt before a workgroup barrier, after which ONE lane
-// adds 1 to the simulation block's counter (a relaxed agent-scope atomic add -- no release
-// fence: the sc1 stores have left the CU once vmcnt drained); the consumer's one lane polls that
-// counter with relaxed agent-scope (sc1) loads, then a workgroup barrier releases the other
-// waves (no acquire fence: every image load bypasses the L1).  Co-residency of the whole grid
-// (one workgroup per CU) is guaranteed by the cooperative launch, which fails instead of
-// running partly resident (the host then falls back to step_kernel).  Every wait is still
-// bounded: a timeout sets the error word, the state is poisoned with NaN, and the host reads
-// the word back and returns WC_EHIP.
-// Double-buffered E image: a block writes E(s+1) into the buffer read at step s-1, which
-// every block of its simulation block has finished reading (it passed that block's step-s
-// wait).  The arithmetic per cell -- K order of the MFMA chain, the epilogue expressions,
-// the noise -- is step_kernel's, so both paths give the same bits.
+// One workgroup (8 waves) owns a tile of 128 nodes x 80 simulations for ALL nsteps steps: wave w
+// holds node tile w (16 nodes) of the five 16-simulation tiles, i.e. 20 (node, sim) cells per lane
+// -- E, I and the a_ie pair in VGPRs, G and the slope per simulation in LDS.  Every step the
+// coupling of its 128 nodes needs the whole E image of its 80 simulations: the K loop (32-node
+// chunks) runs the node block's OWN four chunks first, from LDS (the workgroup's E, written there
+// by its own epilogue; their connectome rows stay resident in LDS), and then the other node blocks'
+// chunks in cyclic order, two chunks (a pair) per workgroup barrier through a 3-stage LDS ring:
+//   * the E image of the remote pairs comes from the workspace with 16-B sc1 buffer loads to
+//     registers, issued TWO pairs ahead (and the first two as soon as the step's hand-off wait is
+//     over, so that their round trip runs under the four local chunks' MFMAs);
+//   * each wave streams its own node tile's connectome rows (read-only) two pairs ahead;
+//   * the order is cyclic from chunk 4 nb for node block nb -- step_kernel accumulates in the same
+//     order, so the two paths agree bit for bit.
+// The epilogue is the packed pair update (cell_pair_f32, two cells per v_pk instruction); the
+// Philox normals of the step are drawn during the local chunks, whose MFMAs leave VALU issue free.
+// Hand-off: MI355X_MICROARCH.md's fence-free form (its "Valid forms" consumer conditions (1)-(4)
+// with row 1 of the sc1 hand-off table, whose store and load cells admit 4-, 8- or 16-B accesses;
+// DESIGN.md 3.1b quotes them): the E image is stored write-through (16-B sc1 buffer stores) and every
+// load of it is a 16-B sc1 buffer load to registers; every storing wave drains vmcnt before a
+// workgroup barrier, after which ONE lane adds 1 to the simulation block's counter (relaxed,
+// agent scope); the consumer's one lane polls that counter with relaxed agent-scope (sc1) loads,
+// then a workgroup barrier releases the other waves.  Co-residency of the whole grid (one workgroup
+// per CU) is guaranteed by the cooperative launch, which fails instead of running partly resident
+// (the host then falls back to step_kernel).  Every wait is bounded: a timeout sets the status word,
+// the state is poisoned with NaN (wc_integrate_status reports it).
+// Double-buffered E image: a block writes E(s+1) into the buffer read at step s-1, which every
+// block of its simulation block has finished reading (it passed that block's step-s wait).
 constexpr int kPN = 128, kPS = 80, kPT = kPS / 16;  // nodes, simulations, simulation tiles per workgroup
 constexpr int kPWaves = kPN / 16;                     // 8
+constexpr int kPLoc = 4;                              // local K chunks (the node block's own nodes)
+constexpr int kPStages = 3;                           // LDS ring of chunk pairs
 constexpr uint32_t kSpinLimit = 1u << 22;             // polls per wait before giving up (~seconds)
 constexpr int kPersistRetry = 1;                      // run_persistent: cooperative launch refused
-#ifndef WC_PPAIR
-#define WC_PPAIR 1
+#ifndef WC_C5_ZEARLY
+#define WC_C5_ZEARLY 0  // 1: the step's normals drawn during the local chunks (0: in the epilogue)
 #endif
-#ifndef WC_PEARLY
-#define WC_PEARLY 1  // the next pair's operand loads issued before the pair's barrier
-#endif
-// K chunks of the connectome tile kept in LDS (112 KB of the 512 KB streamed per step; 8 chunks
-// = 128 KB before the image stages were paired, WC_PPAIR)
-constexpr int kPRes = WC_PPAIR ? 7 : 8;
 
 struct PGeo {
     int B, N, Np, Bp, MT, NC, SBp, NBp;
@@ -730,37 +769,30 @@ struct PArgs {
     PGeo g;
 };
 
-// E image unit (k-chunk c, simulation block sb, part p, simulation tile t): 64 lanes x 16 B,
-// lane (g, j) holding the 8 fp16 values of nodes 16(2c + h) + 4g + r (jj = 4h + r) of
-// simulation 80 sb + 16 t + j -- the MFMA B-operand fragment, so a chunk of a block is 10
-// contiguous KB
-__host__ __device__ __forceinline__ uint32_t pimg_unit(const PGeo& g, int c, int sb, int p, int t) {
-    return (uint32_t)((((size_t)c * g.SBp + sb) * kParts + p) * kPT + t);
-}
-#ifndef WC_PIMG16
-#define WC_PIMG16 1  // the E image in 16-B units of one node tile (hi | lo), one store per lane and tile
-                     // (0: 8-B halves of two tiles per unit; 4.5% slower, profiles/r03_c5_pimg16.log)
-#endif
-// WC_PIMG16 layout: unit (k-chunk c, simulation block sb, simulation tile t, half h) of 64 lanes x
-// 16 B, lane (g, j) holding [hi | lo] of nodes 16 (2c + h) + 4g + r, r < 4, of simulation 80 sb +
-// 16 t + j: the publishing wave (node tile 2c + h) writes whole 16-B pieces, the chunk of a block
-// is still 10 contiguous KB, and the staging splits each piece into the two parts' B fragments
+// E image unit (k-chunk c, simulation block sb, simulation tile t, half h) of 64 lanes x 16 B: lane
+// (g, j) holds [hi | lo] (f16x4 each) of nodes 16 (2c + h) + 4g + r, r < 4, of simulation 80 sb +
+// 16 t + j -- written whole by the wave of node tile 2c + h; the 10 units of a (chunk, simulation
+// block) are 10 contiguous KB, and the staging splits each piece into the two parts' B fragments
 __host__ __device__ __forceinline__ uint32_t pimg_unit16(const PGeo& g, int c, int sb, int t, int h) {
     return (uint32_t)((((size_t)c * g.SBp + sb) * kPT + t) * 2 + h);
 }
 
-// DIAG (timing ablations only, diag build, WCSDE_PERSISTENT=2..7; results are wrong): 1 = no MFMA, 2 = no
-// epilogue arithmetic, 3 = no K-loop operand loads, 4 = no hand-off waits, 5 = no loads for the step's
-// first pair, 6 = no E-image loads (A rows still streamed)
-template <int DIAG = 0>
+// DIAG (timing ablations only, diag build, WCSDE_PERSISTENT=2..5; results are wrong): 1 = no MFMA,
+// 2 = no epilogue arithmetic, 3 = no remote E-image loads (stale stages), 4 = no hand-off waits
+// NRP_T >= 0: the number of remote chunk pairs (NC - 4) / 2 at compile time, the remote K loop
+// fully unrolled (straight-line code keeps the compiler's vmcnt bookkeeping exact: a loop header
+// merges states and waits for every load in flight); -1: a runtime loop, any N
+template <int DIAG = 0, int NRP_T = -1>
 __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a) {
     typedef __attribute__((ext_vector_type(4))) float f4;
     typedef unsigned u2 __attribute__((ext_vector_type(2)));
-    // [stage][part x sim tile][lane] B (2 stages); per-simulation G, slope and keys.  The state and
-    // the A fragments live in registers (~215 VGPRs: one workgroup per CU).
-    // image stages: WC_PPAIR stages the two chunks of a pair behind one barrier (16 per step, not 32)
-    __shared__ f16x8 ldsB[2][WC_PPAIR ? 2 : 1][kParts * kPT][64];
-    __shared__ f16x8 ldsA[kPRes][kPWaves][kParts][64];  // the first kPRes K chunks of the connectome rows, resident
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    // ring of chunk-pair stages [stage][chunk of the pair][part x sim tile][lane] (60 KB): stages 0
+    // and 1 hold the local pairs at the start of a step (written by the epilogue), remote pair k
+    // lands in stage (k + 2) % 3; the local chunks' connectome rows, resident (64 KB)
+    __shared__ f16x8 ldsB[kPStages][2][kParts * kPT][64];
+    __shared__ u2 ldsDummy[256][2];  // stage_pair's unit-less loads land here
+    __shared__ f16x8 ldsA[kPLoc][kPWaves][kParts][64];
     __shared__ float2 ldsGS[kPS];
     __shared__ uint64_t ldsK[kPS];
     __shared__ int go, uni;
@@ -770,13 +802,15 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     pblock(g, sb, nb);
     const int mt = nb * kPWaves + w;  // this wave's node tile
     const int n0 = 16 * mt + 4 * gq;
-    const float* scl = reinterpret_cast<const float*>(a.ws + g.o_scl);
-    const float gscale = scl[1];
+    const int c0 = kPLoc * nb;        // the node block's own chunks: c0 .. c0 + 3
+    const int NRP = NRP_T >= 0 ? NRP_T : (g.NC - kPLoc) / 2;  // remote pairs (NC is a multiple of 4: even)
+    const float gscale = reinterpret_cast<const float*>(a.ws + g.o_scl)[1];
     unsigned* cnt = reinterpret_cast<unsigned*>(a.ws + g.o_cnt) + sb * 16;
     unsigned* err = reinterpret_cast<unsigned*>(a.ws + g.o_err);
-    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(a.ws + g.o_x, 0,
-                                                                         (int)(2 * (size_t)g.Np * g.Bp * 4), 0x00020000);
-    const uint32_t img_units = (uint32_t)((size_t)g.Np * g.Bp * 4 / 1024);  // 1-KB units (64 lanes x 16 B) per image
+    const uint32_t img_bytes = (uint32_t)((size_t)g.Np * g.Bp * 4);
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(a.ws + g.o_x, 0, (int)(2 * img_bytes), 0x00020000);
+    const f16x8* F = reinterpret_cast<const f16x8*>(a.ws + g.o_frag);
+    const f16x8* asrc = F + (size_t)mt * g.NC * kParts * 64 + lane;  // this wave's connectome rows, + c * 128
 
     // ---- state into registers (step_kernel's prep_kernel arithmetic); G and slope per
     // simulation when this workgroup's cells do not vary by node (every sweep but the maps
@@ -789,9 +823,12 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         ldsGS[tid] = b < g.B ? make_float2((float)a.G[(size_t)bb * g.N] * gscale, Tr<float>::slope(a.sigmaE[(size_t)bb * g.N]))
                              : make_float2(0.f, 0.f);
     }
+#pragma unroll
+    for (int i = 0; i < kPLoc; ++i)
+#pragma unroll
+        for (int p = 0; p < kParts; ++p) ldsA[i][w][p][lane] = asrc[(size_t)(c0 + i) * kParts * 64 + p * 64];
     __syncthreads();
-    float E[kPT][4], I[kPT][4];
-    AccA<true> Av[kPT][4];
+    f2v E[kPT][2], I[kPT][2], Ah[kPT][2], Al[kPT][2];  // cells (t, 2q + {0, 1}): nodes n0 + 2q, n0 + 2q + 1
     bool my_uni = true;
 #pragma unroll
     for (int t = 0; t < kPT; ++t) {
@@ -801,50 +838,51 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             const int n = n0 + r;
             const bool ok = b < g.B && n < g.N;
             const size_t o = ok ? (size_t)b * g.N + n : 0;
-            E[t][r] = ok ? (float)a.E[o] : 0.f;
-            I[t][r] = ok ? (float)a.I[o] : 0.f;
-            Av[t][r].set(ok ? a.A[o] : 0.0);
+            AccA<true> acc0;
+            acc0.set(ok ? a.A[o] : 0.0);
+            E[t][r >> 1][r & 1] = ok ? (float)a.E[o] : 0.f;
+            I[t][r >> 1][r & 1] = ok ? (float)a.I[o] : 0.f;
+            Ah[t][r >> 1][r & 1] = acc0.hi;
+            Al[t][r >> 1][r & 1] = acc0.lo;
             if (ok && (a.G[o] != a.G[(size_t)b * g.N] || a.sigmaE[o] != a.sigmaE[(size_t)b * g.N])) my_uni = false;
         }
     }
     if (!my_uni) uni = 0;  // benign race: every writer stores 0
-    // publish this wave's E tiles into image `buf` and signal the simulation block:
-    // write-through (sc1) stores, a vmcnt drain in every storing wave, a workgroup barrier, one
-    // lane's relaxed agent-scope counter add (the fence-free form above: no release fence)
+    const bool pad0 = n0 >= g.N, pad1 = n0 + 1 >= g.N, pad2 = n0 + 2 >= g.N, pad3 = n0 + 3 >= g.N;
+
+    // publish this wave's E tiles into image `buf` (sc1, write-through) and signal the simulation
+    // block; then (after that barrier: every wave has finished reading the ring) write them into the
+    // ring's local stages for this workgroup's next K loop
     auto publish = [&](int buf) {
+        u4 piece[kPT];
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
+            const float ev[4] = {E[t][0].x, E[t][0].y, E[t][1].x, E[t][1].y};
             f16x4 ph[kParts];
-            split2h(E[t], ph[0], ph[1]);
-#if WC_PIMG16
-            typedef unsigned u4s __attribute__((ext_vector_type(4)));
+            split2h(ev, ph[0], ph[1]);
             const u2 h0 = __builtin_bit_cast(u2, ph[0]), h1 = __builtin_bit_cast(u2, ph[1]);
-            const uint32_t unit = buf * img_units + pimg_unit16(g, mt >> 1, sb, t, mt & 1);
-            __builtin_amdgcn_raw_buffer_store_b128(u4s{h0.x, h0.y, h1.x, h1.y}, xrs, (int)((unit * 64 + lane) * 16), 0, 16);
-#else
-#pragma unroll
-            for (int p = 0; p < kParts; ++p) {
-                const uint32_t unit = buf * img_units + pimg_unit(g, mt >> 1, sb, p, t);
-                const int off = (int)((unit * 64 + lane) * 16 + (mt & 1) * 8);
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, ph[p]), xrs, off, 0, 16);
-            }
-#endif
+            piece[t] = u4{h0.x, h0.y, h1.x, h1.y};
+            const uint32_t unit = pimg_unit16(g, mt >> 1, sb, t, mt & 1);
+            __builtin_amdgcn_raw_buffer_store_b128(piece[t], xrs, (int)(buf * img_bytes + (unit * 64 + lane) * 16), 0, 16);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    // consumer: one lane polls the counter (relaxed agent-scope = sc1 loads), then a workgroup
-    // barrier before any wave loads the image, every such load sc1 (no acquire fence; bounded:
-    // error word + exit)
-    auto wait_for = [&](unsigned target) -> bool {
-        if (DIAG == 4) {
-            __syncthreads();
-            return true;
+        // local chunk i = w / 2 (node tiles 2i, 2i + 1 of the block), half h = w % 2: stage i / 2,
+        // chunk-of-pair i % 2 -- the layout the staging gives the remote chunks
+        const int i = w >> 1, hh = w & 1;
+#pragma unroll
+        for (int t = 0; t < kPT; ++t) {
+            *reinterpret_cast<u2*>(reinterpret_cast<unsigned*>(&ldsB[i >> 1][i & 1][t][lane]) + 2 * hh) = u2{piece[t].x, piece[t].y};
+            *reinterpret_cast<u2*>(reinterpret_cast<unsigned*>(&ldsB[i >> 1][i & 1][kPT + t][lane]) + 2 * hh) = u2{piece[t].z, piece[t].w};
         }
+    };
+    // consumer: one lane polls the counter (relaxed agent-scope = sc1 loads); the workgroup barrier
+    // after it releases the other waves (and makes the local stages visible); bounded
+    auto wait_for = [&](unsigned target) -> bool {
         if (tid == 0) {
-            int ok = 0;
-            for (uint32_t it = 0; it < kSpinLimit; ++it) {
+            int ok = DIAG == 4;
+            for (uint32_t it = 0; !ok && it < kSpinLimit; ++it) {
                 if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
                     ok = 1;
                     break;
@@ -860,47 +898,86 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     };
 
     publish(0);
-    bool alive = wait_for((unsigned)g.NBp);
-    const bool uni_wg = uni != 0;  // (the barriers inside publish/wait_for ordered every store to it)
-    const f16x8* F = reinterpret_cast<const f16x8*>(a.ws + g.o_frag);
-    CellConsts kc = a.kc;
-    // the folded constants stay in VGPRs (wave-uniform values; as SGPRs they were spilled to VGPR
-    // lanes and re-read every step)
-    asm volatile("" : "+v"(kc.a_ee), "+v"(kc.Pm), "+v"(kc.rhoE), "+v"(kc.rE), "+v"(kc.rI), "+v"(kc.cIe));
-    asm volatile("" : "+v"(kc.cIi), "+v"(kc.cI0), "+v"(kc.knoise), "+v"(kc.dtE), "+v"(kc.dtI), "+v"(kc.dtA));
+    const bool uni_wg = uni != 0;  // (the barrier inside publish ordered every store to it)
+    const CellConsts kc = a.kc;
+    const CellConsts2 k2 = cell_consts2(kc);
     const size_t BN = (size_t)g.B * g.N;
     int rec_cnt = 0, rec_row = 0;
-    // K loop operands, two chunks ahead, through registers: A = this wave's own node tile (units
-    // 2w, 2w+1 of the read-only connectome image) straight into MFMA fragments; B = the chunk's
-    // 640 E-image units, thread tid loading unit-lane tid (and 512 + tid for tid < 128), written
-    // to one of two LDS stages once they land
-    typedef unsigned u4 __attribute__((ext_vector_type(4)));
-    const f16x8* asrc = F + (size_t)mt * g.NC * kParts * 64 + lane;
-    f16x8 fa[2][kParts];
-    u4 rb[2][2];
-    const int res = g.NC < kPRes ? g.NC : kPRes;  // chunks c < res come from ldsA (NC is a multiple of 4)
-    for (int c = 0; c < res; ++c) {
-        ldsA[c][w][0][lane] = asrc[(size_t)c * kParts * 64];
-        ldsA[c][w][1][lane] = asrc[(size_t)c * kParts * 64 + 64];
+
+    // remote pair k: chunks (c0 + 4 + 2k) % NC and the next; thread tid stages units tid, tid + 512
+    // and (tid < 256) tid + 1024 of the pair's 1280 (out-of-range buffer loads return 0 and move
+    // nothing: every wave issues the same three loads)
+    // Every load of the K loop is issued unconditionally, in the same order every iteration, so that
+    // the compiler's in-order vmcnt bookkeeping stays exact (a load skipped on some path makes it wait
+    // for everything): a load with nothing to fetch gets an out-of-range buffer offset (zeros, no
+    // memory traffic).  Unit q of a pair for thread tid is unit ul = tid + 512 q of its 1280: byte
+    // qo[q] of the image (pair base excluded) and, staged, the LDS bytes qs[q] of a stage (units
+    // beyond 1280, q = 2 for tid >= 256, go to a dummy slot of their own).
+    const uint32_t chunk_bytes = (uint32_t)(g.SBp * (kPT * 2 * 64 * 16));  // one k-chunk of the image
+    const uint32_t sb_off = (uint32_t)(sb * (kPT * 2 * 64 * 16));
+    const uint32_t oob = 2 * img_bytes;
+    uint32_t qo[3], qs[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int ul = tid + 512 * q;
+        const int h = ul >= 640 ? 1 : 0;
+        const int ulc = ul - 640 * h;
+        const int u = ulc >> 6, ln = ulc & 63, t = u >> 1, hh = u & 1;
+        qo[q] = (ul < 1280) ? h * chunk_bytes + ulc * 16 : oob;
+        // byte offset in a stage of the hi half (the lo half is kPT * 1 KB further)
+        qs[q] = (ul < 1280) ? (uint32_t)(((h * kParts * kPT + t) * 64 + ln) * 16 + 8 * hh) : 0u;
     }
-    auto load_chunk = [&](int c, int slot, int buf) {
-        if (DIAG == 3) return;
-        if (c >= res) {
-            const f16x8* ap = asrc + (size_t)c * kParts * 64;
-            fa[slot][0] = ap[0];
-            fa[slot][1] = ap[64];
-        }
-        if (DIAG == 6) return;  // (ablation: no E-image loads, the A rows still streamed)
-        const int xo = (int)(((buf * img_units + pimg_unit(g, c, sb, 0, 0)) * 64 + tid) * 16);
-        rb[slot][0] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 16));
-        if (tid < 128) rb[slot][1] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, xo + 512 * 16, 0, 16));
+    const __amdgpu_buffer_rsrc_t frs =
+        __builtin_amdgcn_make_buffer_rsrc(a.ws + g.o_frag, 0, (int)((size_t)g.MT * g.NC * kParts * 64 * 16), 0x00020000);
+    const uint32_t row_off = (uint32_t)(((size_t)mt * g.NC * kParts * 64 + lane) * 16);  // this wave's rows, chunk 0
+    const uint32_t frag_oob = (uint32_t)((size_t)g.MT * g.NC * kParts * 64 * 16);
+    u4 rb[2][3];
+    f16x8 fa[2][2][kParts];  // rows of the pair [slot][chunk of the pair][part], one pair ahead
+    // chunk index of remote pair k: (c0 + 4 + 2k) mod NC
+    auto rchunk = [&](int k) {
+        const int c = c0 + kPLoc + 2 * k;
+        return c < g.NC ? c : c - g.NC;
     };
-    // chunk c's MFMAs from image stage `st` (each wave reads only its own ldsA slice, written by
-    // itself before the step loop)
-    auto mfma_chunk = [&](int c, f16x8 a0, f16x8 a1, const f16x8 (*stg)[64], f4 (&acc)[kPT]) {
+    auto load_rows = [&](int k, int slot) {
+        const bool live_k = k < NRP;
+        const uint32_t base = row_off + (uint32_t)rchunk(k) * (kParts * 64 * 16);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int p = 0; p < kParts; ++p)
+                fa[slot][h][p] = __builtin_bit_cast(
+                    f16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                               frs, (int)(live_k ? base + (uint32_t)((h * kParts + p) * 64 * 16) : frag_oob), 0, 0));
+    };
+    auto load_pair = [&](int k, int slot, int buf) {
+        const bool live_k = DIAG != 3 && k < NRP;
+        const uint32_t base = buf * img_bytes + (uint32_t)rchunk(k) * chunk_bytes + sb_off;
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+            rb[slot][q] = __builtin_bit_cast(
+                u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)(live_k && qo[q] != oob ? base + qo[q] : oob), 0, 16));
+    };
+    char* const ring = reinterpret_cast<char*>(&ldsB[0][0][0][0]);
+    auto stage_pair = [&](int slot, int st) {
+        if (DIAG == 3) return;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const u4 v = rb[slot][q];
+            char* d = ring + (size_t)st * sizeof(ldsB[0]) + qs[q];
+            char* dl = d + kPT * 64 * 16;
+            if (q == 2) {  // (tid >= 256: no unit; its zeros go to a dummy slot, without a branch)
+                d = tid < 256 ? d : reinterpret_cast<char*>(&ldsDummy[tid & 255][0]);
+                dl = tid < 256 ? dl : reinterpret_cast<char*>(&ldsDummy[tid & 255][1]);
+            }
+            *reinterpret_cast<u2*>(d) = u2{v.x, v.y};
+            *reinterpret_cast<u2*>(dl) = u2{v.z, v.w};
+        }
+    };
+    // the MFMAs of one chunk: A from (a0, a1), B from ring stage st, chunk-of-pair h
+    auto mfma_chunk = [&](f16x8 a0, f16x8 a1, int st, int h, f4 (&acc)[kPT]) {
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
-            const f16x8 fb0 = stg[t][lane], fb1 = stg[kPT + t][lane];
+            const f16x8 fb0 = ldsB[st][h][t][lane], fb1 = ldsB[st][h][kPT + t][lane];
             if (DIAG == 1) {
                 acc[t][0] += (float)fb0[0] + (float)a0[0] + (float)fb1[1] + (float)a1[1];
                 continue;
@@ -911,90 +988,67 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, fb0, acc[t], 0, 0, 0);
         }
     };
-    // WC_PPAIR: chunks c, c + 1 (a pair) staged together into pair stage (c / 2) & 1 behind ONE
-    // barrier; that stage was last read two pairs ago, before the previous pair's barrier.  The
-    // pair's A operands are taken before the next pair's loads overwrite fa.
-    // one staged 16-B unit-lane ul (0..639) of a chunk into ldsB stage `st` (stage row h)
-    auto stage_put = [&](int st, int h, int ul, u4 v) {
-#if WC_PIMG16
-        // unit (t, hh) = ul / 64: hi -> part 0's fragment of tile t, lo -> part 1's, half hh of each
-        const int u = ul >> 6, ln = ul & 63, t = u >> 1, hh = u & 1;
-        unsigned* b0 = reinterpret_cast<unsigned*>(&ldsB[st][h][t][ln]) + 2 * hh;
-        unsigned* b1 = reinterpret_cast<unsigned*>(&ldsB[st][h][kPT + t][ln]) + 2 * hh;
-        *reinterpret_cast<u2*>(b0) = u2{v.x, v.y};
-        *reinterpret_cast<u2*>(b1) = u2{v.z, v.w};
-#else
-        reinterpret_cast<u4*>(&ldsB[st][h][0][0])[ul] = v;
-#endif
-    };
-    auto do_pair = [&](int c, int buf, f4 (&acc)[kPT]) {
-        const int ps = (c >> 1) & 1;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            stage_put(ps, h, tid, rb[h][0]);
-            if (tid < 128) stage_put(ps, h, 512 + tid, rb[h][1]);
-        }
-#if WC_PEARLY
-        // the next pair's loads issued before the barrier (the staged registers are free once
-        // their ds_writes have issued; the A operands of this pair taken first: each wave reads
-        // only its own ldsA slice)
-        const f16x8 a00 = c < res ? ldsA[c][w][0][lane] : fa[0][0];
-        const f16x8 a01 = c < res ? ldsA[c][w][1][lane] : fa[0][1];
-        const f16x8 a10 = c + 1 < res ? ldsA[c + 1][w][0][lane] : fa[1][0];
-        const f16x8 a11 = c + 1 < res ? ldsA[c + 1][w][1][lane] : fa[1][1];
-        if (c + 2 < g.NC) {
-            load_chunk(c + 2, 0, buf);
-            load_chunk(c + 3, 1, buf);
-        }
+    // remote pair k in ring stage st: its E image staged (loaded two pairs ago), one barrier, the
+    // next pair's rows (into the other row slot) and the E image two pairs ahead issued, the MFMAs
+    auto remote_pair = [&](int k, int slot, int st, int buf, f4 (&acc)[kPT]) {
+        stage_pair(slot, st);
         __syncthreads();
-#else
-        __syncthreads();
-        const f16x8 a00 = c < res ? ldsA[c][w][0][lane] : fa[0][0];
-        const f16x8 a01 = c < res ? ldsA[c][w][1][lane] : fa[0][1];
-        const f16x8 a10 = c + 1 < res ? ldsA[c + 1][w][0][lane] : fa[1][0];
-        const f16x8 a11 = c + 1 < res ? ldsA[c + 1][w][1][lane] : fa[1][1];
-        if (c + 2 < g.NC) {
-            load_chunk(c + 2, 0, buf);
-            load_chunk(c + 3, 1, buf);
-        }
-#endif
-        mfma_chunk(c, a00, a01, ldsB[ps][0], acc);
-        mfma_chunk(c + 1, a10, a11, ldsB[ps][1], acc);
+        load_rows(k + 1, slot ^ 1);
+        load_pair(k + 2, slot, buf);
+        mfma_chunk(fa[slot][0][0], fa[slot][0][1], st, 0, acc);
+        mfma_chunk(fa[slot][1][0], fa[slot][1][1], st, 1, acc);
     };
-    auto do_chunk = [&](int c, int slot, int buf, f4 (&acc)[kPT]) {
-        stage_put(slot, 0, tid, rb[slot][0]);
-        if (tid < 128) stage_put(slot, 0, 512 + tid, rb[slot][1]);
-        __syncthreads();  // stage `slot` was last read at chunk c - 2, before the previous barrier
-        // (each wave reads only its own ldsA slice, written by itself before the step loop)
-        const f16x8 a0 = c < res ? ldsA[c][w][0][lane] : fa[slot][0];
-        const f16x8 a1 = c < res ? ldsA[c][w][1][lane] : fa[slot][1];
-        if (c + 2 < g.NC) load_chunk(c + 2, slot, buf);
-        mfma_chunk(c, a0, a1, ldsB[slot][0], acc);
-    };
-    for (int64_t s = 0; s < a.nsteps && alive; ++s) {
+
+    bool alive = true;
+    for (int64_t s = 0; s < a.nsteps; ++s) {
         const int buf = (int)(s & 1);
+        if (!wait_for((unsigned)g.NBp * (unsigned)(s + 1))) {
+            alive = false;
+            break;
+        }
         const bool rec = a.rec_every > 0 && rec_cnt == 0;
         if (a.rec_every > 0) {
             if (rec_cnt == 0) rec_cnt = (int)a.rec_every;
             --rec_cnt;
         }
+        load_pair(0, 0, buf);
+        load_rows(0, 0);
+        load_pair(1, 1, buf);
+        asm volatile("" ::: "memory");  // (the loads stay here, ahead of the local chunks' MFMAs)
         f4 acc[kPT];
 #pragma unroll
         for (int t = 0; t < kPT; ++t) acc[t] = f4{0, 0, 0, 0};
-        if (DIAG != 5) {  // (ablation 5: the step's first pair from stale registers, no exposed round trip)
-            load_chunk(0, 0, buf);
-            load_chunk(1, 1, buf);
-        }
-        for (int c = 0; c < g.NC; c += 2) {  // NC is a multiple of 4 (nodes padded to 128)
-            if (WC_PPAIR) {
-                do_pair(c, buf, acc);
-            } else {
-                do_chunk(c, 0, buf, acc);
-                do_chunk(c + 1, 1, buf, acc);
+        // local chunks (stages 0 and 1, rows from ldsA)
+        const uint64_t gstep = (uint64_t)(a.step0 + s);
+        f2v z[kPT][2];
+        auto noise = [&](int t) {
+            float zz[4];
+            quad_normals_raw(gstep, (uint32_t)(4 * mt + gq), ldsK[16 * t + j], zz);
+            z[t][0] = f2v{zz[0], zz[1]};
+            z[t][1] = f2v{zz[2], zz[3]};
+        };
+#pragma unroll
+        for (int i = 0; i < kPLoc; ++i) {
+            mfma_chunk(ldsA[i][w][0][lane], ldsA[i][w][1][lane], i >> 1, i & 1, acc);
+            if (WC_C5_ZEARLY) {
+                noise(i);
+                if (i == kPLoc - 1) noise(kPT - 1);
             }
         }
-        // ---- epilogue: step_kernel's update on the D fragments (the state in registers) ----
-        const uint64_t gstep = (uint64_t)(a.step0 + s);
+        // remote pairs, two per iteration (the staging and row registers alternate)
+        if constexpr (NRP_T >= 0) {
+#pragma unroll
+            for (int k = 0; k < NRP_T; ++k) remote_pair(k, k & 1, (k + 2) % kPStages, buf, acc);
+        } else {
+            int st = 2;  // remote pair k lands in ring stage (k + 2) mod 3
+            for (int k = 0; k < NRP; k += 2) {
+                remote_pair(k, 0, st, buf, acc);
+                st = st == kPStages - 1 ? 0 : st + 1;
+                remote_pair(k + 1, 1, st, buf, acc);
+                st = st == kPStages - 1 ? 0 : st + 1;
+            }
+        }
+        // ---- epilogue: the packed cell update on the D fragments (the state in registers) ----
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
             __builtin_amdgcn_sched_barrier(0);  // one simulation tile at a time: bounded live ranges
@@ -1012,46 +1066,46 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
                     if (n < Nn) {
                         const size_t cc = (size_t)b * Nn + n;
                         const size_t o = ld ? cc * ld + rec_row : (size_t)rec_row * BN + cc;
-                        static_cast<float*>(a.recE)[o] = E[t][r];
-                        if (a.recI) static_cast<float*>(a.recI)[o] = I[t][r];
-                        if (a.recA) static_cast<float*>(a.recA)[o] = (float)Av[t][r].get();
+                        static_cast<float*>(a.recE)[o] = E[t][r >> 1][r & 1];
+                        if (a.recI) static_cast<float*>(a.recI)[o] = I[t][r >> 1][r & 1];
+                        if (a.recA) static_cast<float*>(a.recA)[o] = (float)((double)Ah[t][r >> 1][r & 1] + (double)Al[t][r >> 1][r & 1]);
                     }
                 }
             }
             if (DIAG == 2) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) E[t][r] += 1e-30f * acc[t][r];
+                for (int q = 0; q < 2; ++q) E[t][q] += 1e-30f * f2v{acc[t][2 * q], acc[t][2 * q + 1]};
                 continue;
             }
-            float z[4];
-            quad_normals_raw(gstep, (uint32_t)(4 * mt + gq), ldsK[16 * t + j], z);
-            float gv[4], sv[4];
+            if (!WC_C5_ZEARLY) noise(t);
+            f2v gv, sv;
+            f2v gv1, sv1;
             if (uni_wg) {
                 const float2 gs = ldsGS[16 * t + j];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    gv[r] = gs.x;
-                    sv[r] = gs.y;
-                }
+                gv = gv1 = f2v{gs.x, gs.x};
+                sv = sv1 = f2v{gs.y, gs.y};
             } else {
+                float gg[4], ss[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int n = n0 + r;
                     const bool ok = live && n < Nn;
                     const size_t o = ok ? (size_t)b * Nn + n : 0;
-                    gv[r] = ok ? (float)a.G[o] * gscale : 0.f;
-                    sv[r] = ok ? Tr<float>::slope(a.sigmaE[o]) : 0.f;
+                    gg[r] = ok ? (float)a.G[o] * gscale : 0.f;
+                    ss[r] = ok ? Tr<float>::slope(a.sigmaE[o]) : 0.f;
                 }
+                gv = f2v{gg[0], gg[1]};
+                gv1 = f2v{gg[2], gg[3]};
+                sv = f2v{ss[0], ss[1]};
+                sv1 = f2v{ss[2], ss[3]};
             }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                cell_update_f32(kc, E[t][r], I[t][r], Av[t][r], acc[t][r], gv[r], sv[r], z[r], n0 + r >= g.N);
+            cell_pair_f32(k2, E[t][0], I[t][0], Ah[t][0], Al[t][0], f2v{acc[t][0], acc[t][1]}, gv, sv, z[t][0], pad0,
+                          pad1);
+            cell_pair_f32(k2, E[t][1], I[t][1], Ah[t][1], Al[t][1], f2v{acc[t][2], acc[t][3]}, gv1, sv1, z[t][1], pad2,
+                          pad3);
         }
         if (rec) ++rec_row;
-        if (s + 1 < a.nsteps) {
-            publish(buf ^ 1);
-            alive = wait_for((unsigned)g.NBp * (unsigned)(s + 2));
-        }
+        if (s + 1 < a.nsteps) publish(buf ^ 1);
     }
     // ---- state back to the caller's fp64 arrays (NaN if a wait timed out) ----
     const bool poisoned = !alive;
@@ -1063,11 +1117,20 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
             const int n = n0 + r;
             if (b < g.B && n < g.N) {
                 const size_t o = (size_t)b * g.N + n;
-                a.E[o] = poisoned ? __builtin_nan("") : (double)E[t][r];
-                a.I[o] = poisoned ? __builtin_nan("") : (double)I[t][r];
-                a.A[o] = poisoned ? __builtin_nan("") : Av[t][r].get();
+                a.E[o] = poisoned ? __builtin_nan("") : (double)E[t][r >> 1][r & 1];
+                a.I[o] = poisoned ? __builtin_nan("") : (double)I[t][r >> 1][r & 1];
+                a.A[o] = poisoned ? __builtin_nan("") : (double)Ah[t][r >> 1][r & 1] + (double)Al[t][r >> 1][r & 1];
             }
         }
+    }
+}
+
+// the kernel for a remote pair count: unrolled for the C5 size (N 897..1024), a runtime loop otherwise
+template <int DIAG>
+const void* persist_for(int nrp) {
+    switch (nrp) {
+        case 14: return (const void*)persist_kernel<DIAG, 14>;
+        default: return (const void*)persist_kernel<DIAG, -1>;
     }
 }
 
@@ -1084,11 +1147,11 @@ int cu_count_large() {
 // (libwcsde_diag.so) 2..5 select the timing ablations (wrong results).
 bool persistent_ok(int B, int N) {
     const char* env = getenv("WCSDE_PERSISTENT");
-    if (env && (env[0] < '1' || env[0] > '7')) return false;
+    if (env && (env[0] < '1' || env[0] > '5')) return false;
     const PGeo g = pgeometry(B, N);
     if (2 * (size_t)g.Np * g.Bp * 4 >= (size_t)INT32_MAX) return false;
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)persist_kernel<0>, kPWaves * 64, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, persist_for<0>((g.NC - kPLoc) / 2), kPWaves * 64, 0) != hipSuccess ||
         occ < 1)
         return false;
     return g.SBp * g.NBp <= cu_count_large();
@@ -1127,23 +1190,29 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
     if (me == hipSuccess) me = hipMemsetAsync(a.ws + g.o_err, 0, 4, st);        // this call's status word
     if (me != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(me));
     const dim3 grid((unsigned)(g.SBp * g.NBp)), blk(kPWaves * 64);
-    const void* kern = (const void*)persist_kernel<0>;
+    const int nrp = (g.NC - kPLoc) / 2;
+    const void* kern = persist_for<0>(nrp);
 #ifdef WCSDE_DIAG
     const char* env = getenv("WCSDE_PERSISTENT");
     switch (env ? env[0] : '1') {
-        case '2': kern = (const void*)persist_kernel<1>; break;
-        case '3': kern = (const void*)persist_kernel<2>; break;
-        case '4': kern = (const void*)persist_kernel<3>; break;
-        case '5': kern = (const void*)persist_kernel<4>; break;
-        case '6': kern = (const void*)persist_kernel<5>; break;
-        case '7': kern = (const void*)persist_kernel<6>; break;
+        case '2': kern = persist_for<1>(nrp); break;
+        case '3': kern = persist_for<2>(nrp); break;
+        case '4': kern = persist_for<3>(nrp); break;
+        case '5': kern = persist_for<4>(nrp); break;
         default: break;
     }
 #endif
     // cooperative: the whole grid is co-resident (the inter-workgroup waits need it) or the launch
     // fails -- e.g. another process holds CUs -- and the caller runs step_kernel instead
     void* kargs[] = {&a};
-    hipError_t e = hipLaunchCooperativeKernel(kern, grid, blk, kargs, 0, st);
+    // WCSDE_COOP=0 (profiling only): an ordinary launch of the same one-workgroup-per-CU grid, all
+    // resident on an otherwise idle GPU; rocprofv3 runs of a process that made a cooperative launch
+    // die in the runtime's teardown, an ordinary launch lets one run hold several
+    // counter passes.  Nothing is guaranteed co-resident then: a wait that cannot be met times out
+    // (status word, NaN state), it does not hang.
+    const char* coop = getenv("WCSDE_COOP");
+    hipError_t e = (coop && coop[0] == '0') ? hipLaunchKernel(kern, grid, blk, kargs, 0, st)
+                                            : hipLaunchCooperativeKernel(kern, grid, blk, kargs, 0, st);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         return kPersistRetry;

@@ -3,6 +3,14 @@
 each, merged back under gpurun_out/prof_c5/), run on the CPU from the repo root:
   profiles/pmc_sde_c5.json  HBM bytes per persist_kernel step, scaled to bench.py's 20,000-step launch
   profiles/pmc_c5_sq.json   instruction mix, MFMA / VALU busy and the wave-cycle split per wave-step"""
+def _dump(d, name):
+    """profiles/<name>, and a copy under gpurun_out/prof_c5/ (the only directory a GPU call returns)."""
+    import json, os
+    json.dump(d, open(os.path.join("profiles", name), "w"), indent=1)
+    os.makedirs("gpurun_out/prof_c5", exist_ok=True)
+    json.dump(d, open(os.path.join("gpurun_out/prof_c5", name), "w"), indent=1)
+
+
 def hbm():
     import json, os, sys
     sys.path.insert(0, "tools")
@@ -25,7 +33,7 @@ def hbm():
                  "dispatch of 400 Euler steps, divided by 400 and scaled by 20,000 to bench.py's per-chunk 'launch'. FETCH_SIZE x2 (gfx950), KB -> B; the "
                  "counters include Infinity-Cache (MALL) hits; the state stays in registers, so the bytes are the "
                  "per-step operand stream (connectome rows and the E image)."}
-    json.dump(d, open("profiles/pmc_sde_c5.json", "w"), indent=1)
+    _dump(d, "pmc_sde_c5.json")
     print(json.dumps(d))
 
 
@@ -48,7 +56,7 @@ def sq():
          "wave_cycle_split": {k: b[k] / b["SQ_WAVE_CYCLES"] for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS")},
          "note": "rocprofv3 --pmc passes of tools/c5_pmc_run.py 400 (one persist_kernel dispatch of 400 Euler steps at the "
                  "C5 shard, 2,500 x 1000, 8 waves per CU on 256 CUs). Busy fractions over GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs."}
-    json.dump(d, open("profiles/pmc_c5_sq.json", "w"), indent=1)
+    _dump(d, "pmc_c5_sq.json")
     print(json.dumps(d))
 
 
@@ -71,7 +79,7 @@ def tcc():
                  "dispatch, 400 steps; tools/profile_c5_pass.sh tcc). unique_operand_bytes_per_step: per XCD the streamed "
                  "connectome rows of its 4 node blocks (25 of 32 K chunks; 7 stay in LDS) plus the E image of its 8 "
                  "simulation blocks, summed over the 8 XCDs (4.2 MB per XCD against a 4 MB L2)."}
-    json.dump(d, open("profiles/pmc_c5_tcc.json", "w"), indent=1)
+    _dump(d, "pmc_c5_tcc.json")
     print(json.dumps(d))
 
 
