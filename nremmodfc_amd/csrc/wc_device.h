@@ -115,6 +115,10 @@ __device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t
 #pragma unroll
     for (int i = 0; i < 4; ++i) z[i] *= kSqrt2Ln2;
 }
+template <typename Coef>
+__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, float z[4], Coef) {
+    quad_normals(step, q, key, z);
+}
 
 // ---------------- fp64 elementary functions for the parity path ----------------
 // Straight-line forms for the inputs this build produces (no special cases, no tables), each
@@ -123,24 +127,70 @@ __device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t
 // ocml's general exp / log / sincospi and the IEEE division sequence took about half of the fp64
 // integrator's VALU.  Coefficients: Taylor series, their truncation below 5e-18 relative.
 namespace f64m {
+// The coefficients, indexed: exp2 [0, 13), log [13, 25) (the last two ln 2 hi and lo), sqrt 2 [25],
+// sin [26, 35), cos [35, 44).  Two ways to read them (the Coef parameter of each function):
+// LitCoef folds them into the code as literals; TabCoef reads them from kCoefDev through a pointer
+// the fp64 integrator launders once per step, so they are scalar loads next to their uses: as
+// literals all ~44 fp64 coefficients are hoisted out of its step loop into ~88 SGPRs and push the
+// kernel's own scalars into VGPR-lane spills re-read by v_readlane every step.
+constexpr double kCoef[44] = {
+    1.3691488853904128e-12, 2.5678435993488206e-11, 4.4455382718708116e-10, 7.054911620801123e-09,
+    1.01780860092397e-07, 1.321548679014431e-06, 1.5252733804059841e-05, 0.0001540353039338161,
+    0.0013333558146428443, 0.009618129107628477, 0.05550410866482158, 0.24022650695910072, 0.6931471805599453,
+    0.09523809523809523, 0.10526315789473684, 0.11764705882352941, 0.13333333333333333, 0.15384615384615385,
+    0.18181818181818182, 0.2222222222222222, 0.2857142857142857, 0.4, 0.6666666666666666,
+    6.93147180369123816490e-01, 1.90821492927058770002e-10,
+    1.4142135623730951,
+    7.952054001475513e-07, -2.1915353447830217e-05, 0.00046630280576761255, -0.0073704309457143504,
+    0.08214588661112823, -0.5992645293207921, 2.5501640398773455, -5.16771278004997, 3.141592653589793,
+    -1.3878952462213771e-07, 4.303069587032947e-06, -0.0001046381049248457, 0.0019295743094039231,
+    -0.02580689139001406, 0.2353306303588932, -1.3352627688545895, 4.0587121264167685, -4.934802200544679};
+__constant__ double kCoefDev[44] = {
+    1.3691488853904128e-12, 2.5678435993488206e-11, 4.4455382718708116e-10, 7.054911620801123e-09,
+    1.01780860092397e-07, 1.321548679014431e-06, 1.5252733804059841e-05, 0.0001540353039338161,
+    0.0013333558146428443, 0.009618129107628477, 0.05550410866482158, 0.24022650695910072, 0.6931471805599453,
+    0.09523809523809523, 0.10526315789473684, 0.11764705882352941, 0.13333333333333333, 0.15384615384615385,
+    0.18181818181818182, 0.2222222222222222, 0.2857142857142857, 0.4, 0.6666666666666666,
+    6.93147180369123816490e-01, 1.90821492927058770002e-10,
+    1.4142135623730951,
+    7.952054001475513e-07, -2.1915353447830217e-05, 0.00046630280576761255, -0.0073704309457143504,
+    0.08214588661112823, -0.5992645293207921, 2.5501640398773455, -5.16771278004997, 3.141592653589793,
+    -1.3878952462213771e-07, 4.303069587032947e-06, -0.0001046381049248457, 0.0019295743094039231,
+    -0.02580689139001406, 0.2353306303588932, -1.3352627688545895, 4.0587121264167685, -4.934802200544679};
+enum : int { kExp = 0, kLog = 13, kLn2Hi = 23, kLn2Lo = 24, kSqrt2 = 25, kSin = 26, kCos = 35 };
+struct LitCoef {
+    __device__ constexpr double operator[](int i) const { return kCoef[i]; }
+    __device__ constexpr LitCoef fresh() const { return *this; }
+};
+typedef __attribute__((address_space(4))) const double* coef_ptr;  // constant address space: scalar loads
+struct TabCoef {
+    coef_ptr p;
+    __device__ double operator[](int i) const { return p[i]; }
+    // a fresh copy of the pointer per function call: its loads cannot be merged with another call's
+    // (each call's coefficients live only in that call)
+    __device__ TabCoef fresh() const {
+        coef_ptr q = p;
+        asm volatile("" : "+s"(q));
+        return TabCoef{q};
+    }
+};
+// TabCoef over kCoefDev with the pointer laundered here (call once per loop iteration)
+__device__ __forceinline__ TabCoef tab_coef() {
+    coef_ptr p = (coef_ptr)kCoefDev;
+    asm volatile("" : "+s"(p));
+    return TabCoef{p};
+}
+
 // 2^t, |t| <= 1000: t = n + r, |r| <= 1/2, e^(r ln 2) to degree 13, scaled by 2^n
-__device__ __forceinline__ double exp2(double t) {
+template <typename Coef = LitCoef>
+__device__ __forceinline__ double exp2(double t, Coef c0 = Coef{}) {
+    const Coef c = c0;
     t = __builtin_fmin(__builtin_fmax(t, -1000.0), 1000.0);
     const double n = __builtin_rint(t);
     const double r = t - n;  // exact
-    double p = 1.3691488853904128e-12;
-    p = __builtin_fma(p, r, 2.5678435993488206e-11);
-    p = __builtin_fma(p, r, 4.4455382718708116e-10);
-    p = __builtin_fma(p, r, 7.054911620801123e-09);
-    p = __builtin_fma(p, r, 1.01780860092397e-07);
-    p = __builtin_fma(p, r, 1.321548679014431e-06);
-    p = __builtin_fma(p, r, 1.5252733804059841e-05);
-    p = __builtin_fma(p, r, 0.0001540353039338161);
-    p = __builtin_fma(p, r, 0.0013333558146428443);
-    p = __builtin_fma(p, r, 0.009618129107628477);
-    p = __builtin_fma(p, r, 0.05550410866482158);
-    p = __builtin_fma(p, r, 0.24022650695910072);
-    p = __builtin_fma(p, r, 0.6931471805599453);
+    double p = c[kExp];
+#pragma unroll
+    for (int i = 1; i < 13; ++i) p = __builtin_fma(p, r, c[kExp + i]);
     p = __builtin_fma(p, r, 1.0);
     return __builtin_ldexp(p, (int)n);
 }
@@ -152,58 +202,61 @@ __device__ __forceinline__ double rcp(double d) {
     e = __builtin_fma(-d, x, 1.0);
     return __builtin_fma(x, e, x);
 }
+// sqrt(x) for a normal positive x (the Box-Muller radius: -2 ln u in [2^-23, 34]): the hardware
+// reciprocal square root and Newton-Raphson on (sqrt, 1/(2 sqrt)) -- the device library's sequence
+// without its denormal scaling and special-value class checks
+__device__ __forceinline__ double sqrt_pos(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double s = x * y, h = 0.5 * y;
+    const double r = __builtin_fma(-s, h, 0.5);
+    s = __builtin_fma(s, r, s);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-s, s, x);
+    s = __builtin_fma(d, h, s);
+    d = __builtin_fma(-s, s, x);
+    return __builtin_fma(d, h, s);
+}
 // ln(v 2^-24) for an odd v < 2^24 (the uniforms u01d): v = f 2^k with f in [1/sqrt2, sqrt2),
-// ln f = 2 atanh(s), s = (f - 1) / (f + 1), |s| <= 0.172, odd series to s^21
-__device__ __forceinline__ double log_u24(uint32_t v) {
+// ln f = 2 atanh(s) = 2 s + s^3 P(s^2), s = (f - 1) / (f + 1), |s| <= 0.172, series to s^21.
+// e ln 2 + 2 s is summed exactly (ln 2 split Cody-Waite style, hi with 32 trailing zero bits so
+// e ln2_hi is exact; Fast2Sum since |e ln 2| >= |2 s| whenever e != 0) and every small term --
+// the quotient's residual, s^3 P, e ln2_lo -- rounds once into the tail: about 0.55 ulp (the
+// single-sum form reached 2.06 ulp where e ln 2 and ln f nearly cancel)
+template <typename Coef = LitCoef>
+__device__ __forceinline__ double log_u24(uint32_t v, Coef c0 = Coef{}) {
+    const Coef c = c0;
     const int k = 31 - __builtin_clz(v);
     double f = __builtin_ldexp((double)v, -k);  // [1, 2), exact
-    const bool hi = f > 1.4142135623730951;
+    const bool hi = f > c[kSqrt2];
     f = hi ? 0.5 * f : f;
     const double e = (double)(k - 24 + (hi ? 1 : 0));
-    // s = (f - 1) / (f + 1) (both exact) to about half an ulp: the product with the reciprocal and
-    // one residual correction (without it the log reached 2.8 ulp where e = 0, v near 2^24)
-    const double num = f - 1.0, den = f + 1.0, rd = rcp(den);
-    double s = num * rd;
-    s = __builtin_fma(__builtin_fma(-s, den, num), rd, s);
+    const double num = f - 1.0, den = f + 1.0, rd = rcp(den);  // num, den exact
+    const double s = num * rd;
+    const double s_lo = __builtin_fma(-s, den, num) * rd;  // s + s_lo = num / den to ~2^-106
     const double s2 = s * s;
-    double p = 0.09523809523809523;
-    p = __builtin_fma(p, s2, 0.10526315789473684);
-    p = __builtin_fma(p, s2, 0.11764705882352941);
-    p = __builtin_fma(p, s2, 0.13333333333333333);
-    p = __builtin_fma(p, s2, 0.15384615384615385);
-    p = __builtin_fma(p, s2, 0.18181818181818182);
-    p = __builtin_fma(p, s2, 0.2222222222222222);
-    p = __builtin_fma(p, s2, 0.2857142857142857);
-    p = __builtin_fma(p, s2, 0.4);
-    p = __builtin_fma(p, s2, 0.6666666666666666);
-    p = __builtin_fma(p, s2, 2.0);
-    return __builtin_fma(e, 0.6931471805599453, __builtin_fma(e, 2.3190468138462996e-17, p * s));
+    double p = c[kLog];
+#pragma unroll
+    for (int i = 1; i < 10; ++i) p = __builtin_fma(p, s2, c[kLog + i]);
+    const double tail = __builtin_fma(s * s2, p, __builtin_fma(e, c[kLn2Lo], 2.0 * s_lo));
+    const double a = e * c[kLn2Hi], b = 2.0 * s;  // both exact
+    const double sum = a + b, err = (a - sum) + b;  // Fast2Sum (a = 0 gives err = 0)
+    return sum + (err + tail);
 }
 // (sin, cos)(pi x) for x = v 2^-23 (v odd, < 2^24: x = 2 u01d): x = n/2 + r, |r| <= 1/4 exactly,
 // sin(pi r) and cos(pi r) to r^17 and r^18, rotated by n quarter turns
-__device__ __forceinline__ void sincospi_v23(uint32_t v, double& sn, double& cs) {
+template <typename Coef = LitCoef>
+__device__ __forceinline__ void sincospi_v23(uint32_t v, double& sn, double& cs, Coef c0 = Coef{}) {
+    const Coef c = c0;
     const uint32_t n = (v + (1u << 21)) >> 22;
     const double r = __builtin_ldexp((double)((int)v - (int)(n << 22)), -23);
     const double r2 = r * r;
-    double ps = 7.952054001475513e-07;
-    ps = __builtin_fma(ps, r2, -2.1915353447830217e-05);
-    ps = __builtin_fma(ps, r2, 0.00046630280576761255);
-    ps = __builtin_fma(ps, r2, -0.0073704309457143504);
-    ps = __builtin_fma(ps, r2, 0.08214588661112823);
-    ps = __builtin_fma(ps, r2, -0.5992645293207921);
-    ps = __builtin_fma(ps, r2, 2.5501640398773455);
-    ps = __builtin_fma(ps, r2, -5.16771278004997);
-    ps = __builtin_fma(ps, r2, 3.141592653589793);
+    double ps = c[kSin];
+#pragma unroll
+    for (int i = 1; i < 9; ++i) ps = __builtin_fma(ps, r2, c[kSin + i]);
     ps *= r;
-    double pc = -1.3878952462213771e-07;
-    pc = __builtin_fma(pc, r2, 4.303069587032947e-06);
-    pc = __builtin_fma(pc, r2, -0.0001046381049248457);
-    pc = __builtin_fma(pc, r2, 0.0019295743094039231);
-    pc = __builtin_fma(pc, r2, -0.02580689139001406);
-    pc = __builtin_fma(pc, r2, 0.2353306303588932);
-    pc = __builtin_fma(pc, r2, -1.3352627688545895);
-    pc = __builtin_fma(pc, r2, 4.0587121264167685);
-    pc = __builtin_fma(pc, r2, -4.934802200544679);
+    double pc = c[kCos];
+#pragma unroll
+    for (int i = 1; i < 9; ++i) pc = __builtin_fma(pc, r2, c[kCos + i]);
     pc = __builtin_fma(pc, r2, 1.0);
     const uint32_t m = n & 3u;
     const double a = (m & 1u) ? pc : ps, b = (m & 1u) ? ps : pc;  // quarter turns: swap
@@ -213,14 +266,15 @@ __device__ __forceinline__ void sincospi_v23(uint32_t v, double& sn, double& cs)
 }  // namespace f64m
 
 // fp64 Box-Muller: sqrt(-2 ln u0) (cos, sin)(2 pi u1) with the straight-line forms above
-__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, double z[4]) {
+template <typename Coef = f64m::LitCoef>
+__device__ __forceinline__ void quad_normals(uint64_t step, uint32_t q, uint64_t key, double z[4], Coef cf = Coef{}) {
     uint32_t x[4];
     philox_ctr(step, q, key, x);
-    const double r0 = sqrt(-2.0 * f64m::log_u24(2u * (x[0] >> 9) + 1u));
-    const double r1 = sqrt(-2.0 * f64m::log_u24(2u * (x[2] >> 9) + 1u));
+    const double r0 = f64m::sqrt_pos(-2.0 * f64m::log_u24(2u * (x[0] >> 9) + 1u, cf));
+    const double r1 = f64m::sqrt_pos(-2.0 * f64m::log_u24(2u * (x[2] >> 9) + 1u, cf));
     double s0, c0, s1, c1;
-    f64m::sincospi_v23(2u * (x[1] >> 9) + 1u, s0, c0);
-    f64m::sincospi_v23(2u * (x[3] >> 9) + 1u, s1, c1);
+    f64m::sincospi_v23(2u * (x[1] >> 9) + 1u, s0, c0, cf);
+    f64m::sincospi_v23(2u * (x[3] >> 9) + 1u, s1, c1, cf);
     z[0] = r0 * c0;
     z[1] = r0 * s0;
     z[2] = r1 * c1;
@@ -238,6 +292,8 @@ template <> struct Tr<float> {
     __device__ static __forceinline__ float sig(float x, float mu, float sl) {
         return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f((mu - x) * sl));
     }
+    template <typename Coef>
+    __device__ static __forceinline__ float sig(float x, float mu, float sl, Coef) { return sig(x, mu, sl); }
     __device__ static __forceinline__ float slope(double s) { return (float)(s * 1.4426950408889634); }
     // C/D row of a 16x16x4 f32 tile is (lane>>4)*4 + reg: identity row->node map
     __host__ __device__ static __forceinline__ int row_node(int rho) { return rho; }
@@ -250,8 +306,9 @@ template <> struct Tr<double> {
     // 1 / (1 + e^(-(x - mu) s)) as 1 / (1 + 2^t), t = (mu - x) s log2(e): exp2 and rcp are within
     // 2 and 1 ulp, but t is rounded first, so the relative error grows as ~2.1 |t| 2^-53 (tens of
     // ulp at |t| ~ 40; tests/test_f64m_gpu.py states the measured bound)
-    __device__ static __forceinline__ double sig(double x, double mu, double s) {
-        return f64m::rcp(1.0 + f64m::exp2((mu - x) * s * 1.4426950408889634));
+    template <typename Coef = f64m::LitCoef>
+    __device__ static __forceinline__ double sig(double x, double mu, double s, Coef c = Coef{}) {
+        return f64m::rcp(1.0 + f64m::exp2((mu - x) * s * 1.4426950408889634, c));
     }
     __device__ static __forceinline__ double slope(double s) { return s; }
     // f64 16x16x4 C/D row is (lane>>4) + 4*reg; permute so that lane group g,

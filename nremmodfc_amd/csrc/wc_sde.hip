@@ -80,6 +80,7 @@ struct KArgs {
     float4* zbuf_next;
     int zgen_b0, zgen_K;
     int64_t zgen_step0;
+    int b0;  // first simulation of this launch (a launch may cover a range of the groups of 16)
 };
 
 // ---------------- A-operand (connectome) images ----------------
@@ -171,6 +172,12 @@ struct PkConsts {
 // hardware reciprocal is exponent-transparent; tools/cmp_libs.py checks the bits).
 // WC_INC2 (default): the a_ie increment as in (E dtA - rhoE dtA), two operations instead of
 // three (WC_INC2=0: the round-2 form in (E tA - rhoE tA), tA = in dtA; -2.5% per C3 launch).
+#ifndef WC_F64_PREGS
+#define WC_F64_PREGS 1
+#endif
+#ifndef WC_F64_TAB
+#define WC_F64_TAB 0  // 1: the fp64 polynomial coefficients as scalar loads from a laundered table pointer
+#endif
 #ifndef WC_INC2
 #define WC_INC2 1
 #endif
@@ -269,7 +276,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr bool kRng = (VAR & V_NO_RNG) == 0;
     constexpr bool kMfma = (VAR & V_NO_MFMA) == 0;
     constexpr bool kPairA = sizeof(Real) == 4 && (VAR & V_KAHAN_A) != 0;
-    constexpr bool kParamRegs = sizeof(Real) == 4;  // fp64 re-reads G/sigmaE (register budget)
+    // G and the slope per cell in registers (fp64: WC_F64_PREGS; else re-read from memory every step)
+    constexpr bool kParamRegs = sizeof(Real) == 4 || WC_F64_PREGS;
     // fp32 with the compensated a_ie: the folded-constant update (Sl holds -sigmaE log2 e)
     constexpr bool kFast = sizeof(Real) == 4 && kPairA;
     constexpr bool kZFirst = kFast && kRng && (VAR & V_ZFIRST) != 0;
@@ -311,7 +319,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     const int lane = threadIdx.x & 63;
     const int w = SG == 1 ? threadIdx.x >> 6 : (threadIdx.x >> 6) % NW;
     const int j = lane & 15, g = lane >> 4;
-    const int b = (blockIdx.x * SG + grp) * kSims + j;
+    const int b = a.b0 + (blockIdx.x * SG + grp) * kSims + j;
     const bool live = b < a.B;
     const int bb = live ? b : a.B - 1;  // tail lanes mirror the last sim, never store
     const int N = a.N;
@@ -768,7 +776,13 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 continue;
             }
             if constexpr (!kHalf) {
-            if constexpr (kRng) quad_normals(gstep, (uint32_t)(4 * TL(u) + g), key, z);
+            // fp64: the polynomial coefficients as scalar loads from a table, the pointer laundered
+            // here so they are not hoisted out of the step loop into SGPRs (f64m, wc_device.h)
+            const auto cf = [] {
+                if constexpr (sizeof(Real) == 8 && WC_F64_TAB) return f64m::tab_coef();
+                else return f64m::LitCoef{};
+            }();
+            if constexpr (kRng) quad_normals(gstep, (uint32_t)(4 * TL(u) + g), key, z, cf);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const Real e = E[u][r], in = I[u][r];
@@ -785,9 +799,9 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                 }
                 const Real cpl = kMfma ? acc[u][r] : e;
                 const Real xE = a_ee * e - ai * in + gc * cpl + P + sqdtD * z[r];
-                const Real SE = Tr<Real>::sig(xE, mu, sl);
+                const Real SE = Tr<Real>::sig(xE, mu, sl, cf);
                 const Real xI = a_ei * e - a_ii * in;
-                const Real SI = Tr<Real>::sig(xI, mu, slI);
+                const Real SI = Tr<Real>::sig(xI, mu, slI, cf);
                 if constexpr (sizeof(Real) == 8) {
                     // (the divisions by the time constants as a product with the reciprocal plus one
                     // correction step: the quotient to within an ulp, without the IEEE sequence)
@@ -905,7 +919,7 @@ int tiles_for(int N) { return (N + 15) / 16; }
 
 template <typename Real, int NT, int NW, int VAR, int MINW = 1, int SG = 1>
 int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st, bool prep = true, int extra_blocks = 0,
-             size_t lds_floor = 0) {
+             size_t lds_floor = 0, int g0 = 0, int ng = -1) {
     constexpr bool hf = (VAR & V_F16X3) != 0;
     constexpr bool bf = (VAR & (V_BF16X6 | V_BF16X3)) != 0;
     constexpr bool frag_regs = (VAR & V_FRAG_REGS) != 0;
@@ -928,19 +942,24 @@ int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st, bool p
               (NW > 1 ? (size_t)SG * 2 * (NT / 2) * 3 * 64 * 16 : 0);
     } else {
         const int total = NT * NT * 64 * 4;
-        hipLaunchKernelGGL((build_frag<Real, NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
-                           static_cast<Real*>(ws));
+        if (prep)
+            hipLaunchKernelGGL((build_frag<Real, NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
+                               static_cast<Real*>(ws));
         lds = (frag_regs ? 0 : (size_t)NT * NT * 64 * 4 * sizeof(Real)) +
               (NW > 1 ? (size_t)SG * 2 * NT * 64 * 4 * sizeof(Real) : 0);
     }
-    const int blocks = (ka.B + kSims * SG - 1) / (kSims * SG) + extra_blocks;
+    // groups of 16 simulations g0 .. g0 + ng - 1 (ng < 0: to the last)
+    KArgs kl = ka;
+    kl.b0 = g0 * kSims;
+    if (ng < 0) ng = (ka.B + kSims - 1) / kSims - g0;
+    const int blocks = (ng + SG - 1) / SG + extra_blocks;
     lds = std::max(lds, lds_floor);  // (a floor above half the CU's LDS: one workgroup per CU)
     auto kern = wc_sde_kernel<Real, NT, NW, VAR, MINW, SG>;
     if (lds > 65536) {
         hipError_t ea = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
     }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(NW * 64 * SG), lds, st, ka);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(NW * 64 * SG), lds, st, kl);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(e));
     return WC_OK;
@@ -948,7 +967,10 @@ int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st, bool p
 
 // ---------------- product configurations ----------------
 constexpr int kVarF32 = V_F16X3 | V_FRAG_REGS | V_KAHAN_A;
-constexpr int kVarF64 = 0;
+#ifndef WC_F64_VAR_EXTRA
+#define WC_F64_VAR_EXTRA 0  // ablation builds only (e.g. V_NO_MFMA, V_NO_RNG)
+#endif
+constexpr int kVarF64 = WC_F64_VAR_EXTRA;
 
 size_t frag_bytes(int N, int precision) {
     if (precision == WC_F64) {
@@ -1097,6 +1119,26 @@ int launch_f32(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
 #ifndef WC_F64_SG
 #define WC_F64_SG 2
 #endif
+#ifndef WC_F64_TAIL
+#define WC_F64_TAIL 1
+#endif
+// N 81..96: WC_F64_SG groups of 16 simulations per workgroup share one LDS copy of the fp64
+// connectome image (73.7 KB), one workgroup per CU.  The groups left over after the full rounds of
+// WC_F64_SG x CUs, when they fit one group per CU, run as a second launch of one-group workgroups
+// (WC_F64_TAIL): a CU's step with six waves takes ~0.7 of the two-group step, so the last round
+// costs that instead of a whole round (1,250 groups on 256 CUs: two full rounds + 226 groups)
+int launch_f64_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
+    constexpr int SG = WC_F64_SG;
+    const int groups = (ka.B + kSims - 1) / kSims, cus = cu_count();
+    const int rem = groups % (SG * cus), full = groups - rem;
+    if (SG == 1 || !WC_F64_TAIL || rem == 0 || rem > cus)
+        return launch_v<double, 6, 6, kVarF64, 1, SG>(ka, sc, ws, st);
+    if (full > 0) {
+        const int rc = launch_v<double, 6, 6, kVarF64, 1, SG>(ka, sc, ws, st, true, 0, 0, 0, full);
+        if (rc != WC_OK) return rc;
+    }
+    return launch_v<double, 6, 6, kVarF64, 1, 1>(ka, sc, ws, st, full == 0, 0, 0, full, rem);
+}
 int launch_f64(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     switch (tiles_for(ka.N)) {
         case 1: return launch_v<double, 1, 1, kVarF64>(ka, sc, ws, st);
@@ -1104,9 +1146,7 @@ int launch_f64(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
         case 3: return launch_v<double, 3, 3, kVarF64>(ka, sc, ws, st);
         case 4: return launch_v<double, 4, 4, kVarF64>(ka, sc, ws, st);
         case 5: return launch_v<double, 5, 5, kVarF64>(ka, sc, ws, st);
-        // N 81..96: WC_F64_SG groups of 16 simulations per workgroup share one LDS copy of the fp64
-        // connectome image (73.7 KB): 2 groups (12 waves) per CU instead of one
-        case 6: return launch_v<double, 6, 6, kVarF64, 1, WC_F64_SG>(ka, sc, ws, st);
+        case 6: return launch_f64_nt6(ka, sc, ws, st);
         default: return wc_set_err(WC_EUNSUPPORTED, "N > 96 not supported by the register-resident kernel");
     }
 }
@@ -1207,6 +1247,7 @@ int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const 
     ka.step0 = step0; ka.rec_every = rec_every; ka.rec_ld = rec_ld; ka.nsteps = (int)nsteps; ka.B = B; ka.N = N;
     ka.zbuf = nullptr;
     ka.zBp = 0;
+    ka.b0 = 0;
     if (precision == WC_F32 && zmem_eligible_shape(B, N) && ws_bytes >= zmem_offset(N) + 2 * zmem_block_bytes(B))
         ka.zbuf = reinterpret_cast<const float4*>(static_cast<char*>(workspace) + zmem_offset(N));
     return WC_OK;
@@ -1215,7 +1256,7 @@ int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const 
 #ifdef WCSDE_DIAG
 // the fp64 parity path's straight-line elementary functions (wc_device.h, f64m), evaluated alone
 // for tests/test_f64m_gpu.py: 0 exp2(t), 1 rcp(d), 2 log_u24(v), 3 sincospi_v23(v) -> (sin, cos),
-// 4 the fp64 sigmoid Tr<double>::sig(x, mu = 1, s) of (x, s) pairs
+// 4 the fp64 sigmoid Tr<double>::sig(x, mu = 1, s) of (x, s) pairs, 5 sqrt_pos(x)
 __global__ void f64m_kernel(int fn, int64_t n, const void* __restrict__ in, double* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1226,6 +1267,7 @@ __global__ void f64m_kernel(int fn, int64_t n, const void* __restrict__ in, doub
         case 1: out[i] = f64m::rcp(d[i]); break;
         case 2: out[i] = f64m::log_u24(u[i]); break;
         case 3: f64m::sincospi_v23(u[i], out[2 * i], out[2 * i + 1]); break;
+        case 5: out[i] = f64m::sqrt_pos(d[i]); break;
         default: out[i] = Tr<double>::sig(d[2 * i], 1.0, d[2 * i + 1]); break;
     }
 }
@@ -1305,7 +1347,7 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
 
 int wc_diag_f64m(int fn, int64_t n, const void* in, double* out, void* stream) {
     wc_clear_err();
-    if (fn < 0 || fn > 4 || n <= 0 || n > (int64_t(1) << 30) || !in || !out)
+    if (fn < 0 || fn > 5 || n <= 0 || n > (int64_t(1) << 30) || !in || !out)
         return wc_set_err(WC_EINVAL, "wc_diag_f64m: bad arguments");
     hipLaunchKernelGGL(f64m_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                        fn, n, in, out);

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <type_traits>
 #include "wc_common.h"
 #include "wc_device.h"
 
@@ -686,9 +687,6 @@ constexpr int kPLoc = 4;                              // local K chunks (the nod
 constexpr int kPStages = 3;                           // LDS ring of chunk pairs
 constexpr uint32_t kSpinLimit = 1u << 22;             // polls per wait before giving up (~seconds)
 constexpr int kPersistRetry = 1;                      // run_persistent: cooperative launch refused
-#ifndef WC_C5_ZEARLY
-#define WC_C5_ZEARLY 0  // 1: the step's normals drawn during the local chunks (0: in the epilogue)
-#endif
 
 struct PGeo {
     int B, N, Np, Bp, MT, NC, SBp, NBp;
@@ -916,6 +914,10 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     const uint32_t chunk_bytes = (uint32_t)(g.SBp * (kPT * 2 * 64 * 16));  // one k-chunk of the image
     const uint32_t sb_off = (uint32_t)(sb * (kPT * 2 * 64 * 16));
     const uint32_t oob = 2 * img_bytes;
+    // (lanes 2m and 2m + 1 take the two halves hh of the same (tile, lane): their 8-B LDS writes are
+    // 16 contiguous bytes, so a 16-lane group of ds_write_b64 covers 32 banks once -- the plain
+    // lane-linear order put lanes l and l + 8 on one bank; in global memory the wave's loads are
+    // two 512-B runs instead of one 1-KB run)
     uint32_t qo[3], qs[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -1030,10 +1032,6 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
 #pragma unroll
         for (int i = 0; i < kPLoc; ++i) {
             mfma_chunk(ldsA[i][w][0][lane], ldsA[i][w][1][lane], i >> 1, i & 1, acc);
-            if (WC_C5_ZEARLY) {
-                noise(i);
-                if (i == kPLoc - 1) noise(kPT - 1);
-            }
         }
         // remote pairs, two per iteration (the staging and row registers alternate)
         if constexpr (NRP_T >= 0) {
@@ -1077,7 +1075,7 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
                 for (int q = 0; q < 2; ++q) E[t][q] += 1e-30f * f2v{acc[t][2 * q], acc[t][2 * q + 1]};
                 continue;
             }
-            if (!WC_C5_ZEARLY) noise(t);
+            noise(t);
             f2v gv, sv;
             f2v gv1, sv1;
             if (uni_wg) {
@@ -1125,7 +1123,7 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     }
 }
 
-// the kernel for a remote pair count: unrolled for the C5 size (N 897..1024), a runtime loop otherwise
+constexpr int kPThreads = kPWaves * 64;
 template <int DIAG>
 const void* persist_for(int nrp) {
     switch (nrp) {
@@ -1151,7 +1149,7 @@ bool persistent_ok(int B, int N) {
     const PGeo g = pgeometry(B, N);
     if (2 * (size_t)g.Np * g.Bp * 4 >= (size_t)INT32_MAX) return false;
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, persist_for<0>((g.NC - kPLoc) / 2), kPWaves * 64, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, persist_for<0>((g.NC - kPLoc) / 2), kPThreads, 0) != hipSuccess ||
         occ < 1)
         return false;
     return g.SBp * g.NBp <= cu_count_large();
@@ -1189,7 +1187,7 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
     hipError_t me = hipMemsetAsync(a.ws + g.o_cnt, 0, g.total - g.o_cnt, st);  // counters
     if (me == hipSuccess) me = hipMemsetAsync(a.ws + g.o_err, 0, 4, st);        // this call's status word
     if (me != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(me));
-    const dim3 grid((unsigned)(g.SBp * g.NBp)), blk(kPWaves * 64);
+    const dim3 grid((unsigned)(g.SBp * g.NBp)), blk(kPThreads);
     const int nrp = (g.NC - kPLoc) / 2;
     const void* kern = persist_for<0>(nrp);
 #ifdef WCSDE_DIAG

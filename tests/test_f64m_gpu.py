@@ -8,7 +8,7 @@ oracle, 6e-15 against the reference's own run() under noise replay) is in test_s
 pins each function alone with an explicit ulp bound:
 
 * log_u24 and sincospi_v23 over ALL 2^23 odd v < 2^24 (every uniform the noise stream can give);
-* exp2 over the clamp range and densely over |t| <= 80; rcp over positive normals;
+* exp2 over the clamp range and densely over |t| <= 80; rcp and sqrt_pos over positive normals;
 * the fp64 sigmoid 1 / (1 + 2^t), t = (mu - x) s log2(e): its relative error grows with |t|, because t
   is rounded before the exponential (about 2.08 |t| units of 2^-53 from the three roundings of t; at
   |t| = 40 that is ~80 units, tens of ulp) -- the bound below states exactly that.
@@ -92,6 +92,17 @@ def test_exp2_and_rcp(diag):
     got = _run(diag, 1, d, len(d))
     u = _ulps(got, 1 / d.astype(np.longdouble))
     print(f"TOL rcp: max {u.max():.3f} ulp (bound 1)")
+    assert u.max() <= 1.0
+
+
+def test_sqrt_pos(diag):
+    """The Box-Muller radius sqrt(-2 ln u) without the library's scaling: over the whole range of
+    -2 ln u for 24-bit uniforms, [2^-23, 33.3], and beyond."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([np.exp(rng.uniform(np.log(2.0 ** -24), np.log(40.0), 1 << 20)), [2.0 ** -23, 33.27]])
+    got = _run(diag, 5, x, len(x))
+    u = _ulps(got, np.sqrt(x.astype(np.longdouble)))
+    print(f"TOL sqrt_pos: max {u.max():.3f} ulp (bound 1)")
     assert u.max() <= 1.0
 
 
