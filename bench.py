@@ -372,7 +372,8 @@ def main():
             pmc_refused.append({"file": os.path.relpath(path, ROOT), "stamp": d.get("lib_sha256"), "loaded": stamp})
             return {}
         return d
-    pmc = os.path.join(ROOT, "profiles", "pmc_sde.json" if args.config == "c3" else "pmc_sde_c5.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_sde_c5.json" if args.config != "c3" else
+                       "pmc_sde.json" if args.precision == "f32" else "pmc_sde_f64.json")
     d = stamped(pmc)
     if d.get("B") == B and d.get("N") == N and d.get("euler_steps") == EULER and \
             d.get("precision") == args.precision and \
@@ -388,6 +389,10 @@ def main():
             util.update({k: q[k] for k in ("mfma_busy_frac", "valu_issue_busy_frac", "salu_per_wave_step") if k in q})
             util.update({f"{k.lower()}_per_wave_step": v for k, v in q.get("per_wave_step", {}).items()})
             util["wave_cycle_split"] = q.get("wave_cycle_split")
+    if args.precision == "f64" and pmc_d:
+        # the fp64 integrator's SQ passes (tools/profile_f64.sh)
+        util.update({k: pmc_d[k] for k in ("mfma_busy_frac", "valu_issue_busy_frac", "wave_cycle_split") if k in pmc_d})
+        util.update({f"{k.lower()}_per_wave_step": v for k, v in pmc_d.get("per_wave_step", {}).items()})
     sq = pmc_d.get("sq", {})
     if sq.get("SQ_ACTIVE_INST_VALU") and sq.get("GRBM_GUI_ACTIVE"):
         # SQ_ACTIVE_INST_VALU counts quad-cycles per SIMD; GRBM_GUI_ACTIVE sums the 8 XCDs' clocks
@@ -397,7 +402,29 @@ def main():
         ifl = issued_mfma_flops_per_node_step(N)
         issued = {"dtype": "f16", "flops_per_node_step": ifl, "tflops": per_launch_ns * ifl / t_launch / 1e12,
                   "peak": PEAK_F16_TFLOPS, "util": per_launch_ns * ifl / t_launch / 1e12 / PEAK_F16_TFLOPS}
-    if N <= 96:
+    if N <= 96 and args.precision == "f64":
+        # the fp64 parity integrator (wc_sde_kernel<double>): per SIMD the fp64 VALU work and the fp64 MFMA
+        # coupling take turns (ablations, DESIGN.md 5: no MFMA -105 ms, no normals -77 ms of 293), so the
+        # bound is their summed issue time: 4 cycles per fp64 VALU instruction, 64 per v_mfma_f64_16x16x4
+        # (78.6 TFLOP/s over 1024 SIMDs at 2.4 GHz), over the wave-steps of the launch
+        achieved = per_launch_ns * fl / t_launch / 1e12
+        roof = {"bound": "valu+mfma (fp64)", "achieved": achieved, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / PEAK_FP64_TFLOPS, "traffic": traffic,
+                "traffic_algorithmic": B * N * (EULER // R * 8 + 2 * 3 * 8 + 2 * 8),
+                "kernel": "wc_sde_kernel<double> (one launch = %d Euler steps of %d sims; the full two-group "
+                          "rounds and the one-group tail are two dispatches)" % (EULER, B),
+                "algorithmic_flops_per_node_step": fl,
+                "issued_fp64_mfma_flops_per_node_step": 2 * 96 * 96 / N if N > 80 else None,
+                "note": "frac = algorithmic flops / fp64 vector peak (78.6 TFLOP/s, = the fp64 MFMA peak on MI355X); "
+                        "issue_model prices the instructions the kernel issues (PMC) at the fp64 pipe rates"}
+        pws = pmc_d.get("per_wave_step", {})
+        if pws.get("SQ_INSTS_VALU") and pws.get("SQ_INSTS_MFMA"):
+            wave_steps = -(-B // 16) * 6 * EULER
+            cyc = 4 * pws["SQ_INSTS_VALU"] + 64 * pws["SQ_INSTS_MFMA"]
+            t_model = wave_steps * cyc / 1024 / 2.4e9
+            roof["issue_model"] = {"cycles_per_wave_step": cyc, "wave_steps": wave_steps,
+                                   "ms_all_simds_busy": t_model * 1e3, "frac": t_model / t_launch}
+    elif N <= 96:
         # C3 (wc_sde_kernel): state in registers for the whole launch; PMC: VALU-issue-bound (MFMA busy ~15 %).
         # SURVEY 8(d)'s algorithmic work F(N) = 2N + 35 flops per node-step against the fp32 VECTOR (VALU) peak.
         peak = PEAK_FP32_TFLOPS if args.precision == "f32" else PEAK_FP64_TFLOPS
