@@ -667,8 +667,8 @@ int run_large(const wc_params* p, int B, int N, const double* sc, const double* 
 //   * each wave streams its own node tile's connectome rows (read-only) two pairs ahead;
 //   * the order is cyclic from chunk 4 nb for node block nb -- step_kernel accumulates in the same
 //     order, so the two paths agree bit for bit.
-// The epilogue is the packed pair update (cell_pair_f32, two cells per v_pk instruction); the
-// Philox normals of the step are drawn during the local chunks, whose MFMAs leave VALU issue free.
+// The epilogue is the packed pair update (cell_pair_f32, two cells per v_pk instruction), the
+// step's Philox normals drawn there per simulation tile.
 // Hand-off: MI355X_MICROARCH.md's fence-free form (its "Valid forms" consumer conditions (1)-(4)
 // with row 1 of the sc1 hand-off table, whose store and load cells admit 4-, 8- or 16-B accesses;
 // DESIGN.md 3.1b quotes them): the E image is stored write-through (16-B sc1 buffer stores) and every
@@ -898,7 +898,10 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     publish(0);
     const bool uni_wg = uni != 0;  // (the barrier inside publish ordered every store to it)
     const CellConsts kc = a.kc;
-    const CellConsts2 k2 = cell_consts2(kc);
+    CellConsts2 k2 = cell_consts2(kc);
+    // the packed cell constants pinned in VGPR pairs (as SGPR pairs they crowd the scalar file, see rchunk)
+    asm volatile("" : "+v"(k2.a_ee), "+v"(k2.Pm), "+v"(k2.cIe), "+v"(k2.cIi), "+v"(k2.cI0), "+v"(k2.knoise));
+    asm volatile("" : "+v"(k2.dtE), "+v"(k2.dtI), "+v"(k2.dtA), "+v"(k2.cA), "+v"(k2.nrE), "+v"(k2.nrI));
     const size_t BN = (size_t)g.B * g.N;
     int rec_cnt = 0, rec_row = 0;
 
@@ -914,10 +917,8 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     const uint32_t chunk_bytes = (uint32_t)(g.SBp * (kPT * 2 * 64 * 16));  // one k-chunk of the image
     const uint32_t sb_off = (uint32_t)(sb * (kPT * 2 * 64 * 16));
     const uint32_t oob = 2 * img_bytes;
-    // (lanes 2m and 2m + 1 take the two halves hh of the same (tile, lane): their 8-B LDS writes are
-    // 16 contiguous bytes, so a 16-lane group of ds_write_b64 covers 32 banks once -- the plain
-    // lane-linear order put lanes l and l + 8 on one bank; in global memory the wave's loads are
-    // two 512-B runs instead of one 1-KB run)
+    // (lane-linear: a wave loads one contiguous 1-KB unit; pairing a thread's units as the two 8-B
+    // halves of one LDS slot was slower, docs/CHANGELOG.md round 5)
     uint32_t qo[3], qs[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -933,31 +934,38 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         __builtin_amdgcn_make_buffer_rsrc(a.ws + g.o_frag, 0, (int)((size_t)g.MT * g.NC * kParts * 64 * 16), 0x00020000);
     const uint32_t row_off = (uint32_t)(((size_t)mt * g.NC * kParts * 64 + lane) * 16);  // this wave's rows, chunk 0
     const uint32_t frag_oob = (uint32_t)((size_t)g.MT * g.NC * kParts * 64 * 16);
-    u4 rb[2][3];
+    constexpr int kLead = 2;  // remote pairs whose E image is in flight in registers
+    u4 rb[kLead][3];
     f16x8 fa[2][2][kParts];  // rows of the pair [slot][chunk of the pair][part], one pair ahead
-    // chunk index of remote pair k: (c0 + 4 + 2k) mod NC
+    // chunk index of remote pair k: (c0 + 4 + 2k) mod NC.  Its inputs are laundered at the top of
+    // every step: as step-invariants the unrolled loop's ~30 per-pair offsets are hoisted into SGPRs,
+    // overflow the file and push the buffer descriptors into VGPR lanes, re-read by 16 v_readlane
+    // before every load group (313 readlanes per step before, 27 after, with the constants above)
+    int c0v = c0, ncv = g.NC;
+    uint32_t cbv = chunk_bytes, sbv = sb_off;
     auto rchunk = [&](int k) {
-        const int c = c0 + kPLoc + 2 * k;
-        return c < g.NC ? c : c - g.NC;
+        const int c = c0v + kPLoc + 2 * k;
+        return c < ncv ? c : c - ncv;
     };
+    // (the pair's uniform base goes in the SGPR offset operand and the lane's part in the VGPR one, so
+    // an address costs no VALU; a pair past the last, k >= NRP, loads from an out-of-range offset)
     auto load_rows = [&](int k, int slot) {
         const bool live_k = k < NRP;
-        const uint32_t base = row_off + (uint32_t)rchunk(k) * (kParts * 64 * 16);
+        const int so = live_k ? (int)((uint32_t)rchunk(k) * (kParts * 64 * 16)) : 0;
+        const uint32_t vo = live_k ? row_off : frag_oob;
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int p = 0; p < kParts; ++p)
                 fa[slot][h][p] = __builtin_bit_cast(
-                    f16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                               frs, (int)(live_k ? base + (uint32_t)((h * kParts + p) * 64 * 16) : frag_oob), 0, 0));
+                    f16x8, __builtin_amdgcn_raw_buffer_load_b128(frs, (int)(vo + (uint32_t)((h * kParts + p) * 64 * 16)), so, 0));
     };
     auto load_pair = [&](int k, int slot, int buf) {
         const bool live_k = DIAG != 3 && k < NRP;
-        const uint32_t base = buf * img_bytes + (uint32_t)rchunk(k) * chunk_bytes + sb_off;
+        const int so = live_k ? (int)(buf * img_bytes + (uint32_t)rchunk(k) * cbv + sbv) : 0;
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-            rb[slot][q] = __builtin_bit_cast(
-                u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)(live_k && qo[q] != oob ? base + qo[q] : oob), 0, 16));
+            rb[slot][q] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xrs, (int)(live_k ? qo[q] : oob), so, 16));
     };
     char* const ring = reinterpret_cast<char*>(&ldsB[0][0][0][0]);
     auto stage_pair = [&](int slot, int st) {
@@ -992,18 +1000,20 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     };
     // remote pair k in ring stage st: its E image staged (loaded two pairs ago), one barrier, the
     // next pair's rows (into the other row slot) and the E image two pairs ahead issued, the MFMAs
-    auto remote_pair = [&](int k, int slot, int st, int buf, f4 (&acc)[kPT]) {
-        stage_pair(slot, st);
+    // (E-image register slot es = k mod kLead, row slot rs = k mod 2)
+    auto remote_pair = [&](int k, int es, int rs, int st, int buf, f4 (&acc)[kPT]) {
+        stage_pair(es, st);
         __syncthreads();
-        load_rows(k + 1, slot ^ 1);
-        load_pair(k + 2, slot, buf);
-        mfma_chunk(fa[slot][0][0], fa[slot][0][1], st, 0, acc);
-        mfma_chunk(fa[slot][1][0], fa[slot][1][1], st, 1, acc);
+        load_rows(k + 1, rs ^ 1);
+        load_pair(k + kLead, es, buf);
+        mfma_chunk(fa[rs][0][0], fa[rs][0][1], st, 0, acc);
+        mfma_chunk(fa[rs][1][0], fa[rs][1][1], st, 1, acc);
     };
 
     bool alive = true;
     for (int64_t s = 0; s < a.nsteps; ++s) {
         const int buf = (int)(s & 1);
+        asm volatile("" : "+s"(c0v), "+s"(ncv), "+s"(cbv), "+s"(sbv));
         if (!wait_for((unsigned)g.NBp * (unsigned)(s + 1))) {
             alive = false;
             break;
@@ -1015,7 +1025,8 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         }
         load_pair(0, 0, buf);
         load_rows(0, 0);
-        load_pair(1, 1, buf);
+#pragma unroll
+        for (int k = 1; k < kLead; ++k) load_pair(k, k, buf);
         asm volatile("" ::: "memory");  // (the loads stay here, ahead of the local chunks' MFMAs)
         f4 acc[kPT];
 #pragma unroll
@@ -1036,13 +1047,13 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
         // remote pairs, two per iteration (the staging and row registers alternate)
         if constexpr (NRP_T >= 0) {
 #pragma unroll
-            for (int k = 0; k < NRP_T; ++k) remote_pair(k, k & 1, (k + 2) % kPStages, buf, acc);
+            for (int k = 0; k < NRP_T; ++k) remote_pair(k, k % kLead, k & 1, (k + 2) % kPStages, buf, acc);
         } else {
             int st = 2;  // remote pair k lands in ring stage (k + 2) mod 3
             for (int k = 0; k < NRP; k += 2) {
-                remote_pair(k, 0, st, buf, acc);
+                remote_pair(k, 0, 0, st, buf, acc);
                 st = st == kPStages - 1 ? 0 : st + 1;
-                remote_pair(k + 1, 1, st, buf, acc);
+                remote_pair(k + 1, 1, 1, st, buf, acc);
                 st = st == kPStages - 1 ? 0 : st + 1;
             }
         }
