@@ -87,3 +87,6 @@ cp $OUT/bench_kernel_stats.csv gpurun_out/prof/r03_bench_kernel_stats.csv 2>/dev
 # on the GPU box only gpurun_out/ travels back: copy gpurun_out/prof/pmc_sde.json and
 # gpurun_out/prof/bench_kernel_stats.csv into profiles/ afterwards
 tail -1 $OUT/trace.log
+# per-dispatch CSVs stay on the box (a call returns at most 64 MiB of gpurun_out/)
+find $OUT -name "*counter_collection.csv" -delete
+find $OUT -name "*kernel_trace.csv" -delete

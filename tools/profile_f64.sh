@@ -43,3 +43,5 @@ d = {"kernel": " + ".join(sorted(sa)), "lib_sha256": stamp, "B": B, "N": 90, "eu
 json.dump(d, open("gpurun_out/prof64/pmc_sde_f64.json", "w"), indent=1)
 print(json.dumps(d))
 PY
+find gpurun_out/prof64 -name "*counter_collection.csv" -delete
+find gpurun_out/prof64 -name "*kernel_trace.csv" -delete
