@@ -5,13 +5,16 @@
 # included) runs as SLURM-array task 0 of W; each task prints its wall time (the perf JSON line).
 # The W-GPU sweep time is the slowest shard's time (the shards are equal to one simulation), so
 # the projected speed-up at W is t(1) / t(W).  Not a SCALE run: one GPU, one shard at a time.
+# MODE="maps --map-ids 1 1" (or "2 2") projects the C4 heterogeneity sweeps the same way.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/shards
+MODE=${MODE:-homo}
+OUT=${OUT:-gpurun_out/shards}
+export OUT
 mkdir -p $OUT
 for W in ${WS:-1 2 4 8 16}; do
   rm -rf $OUT/w$W
   SLURM_ARRAY_TASK_ID=0 SLURM_ARRAY_TASK_MAX=$((W - 1)) timeout -k 10 300 \
-    python -m nremmodfc_amd.sweep homo --out $OUT/w$W > $OUT/w$W.log 2>&1
+    python -m nremmodfc_amd.sweep $MODE --out $OUT/w$W > $OUT/w$W.log 2>&1
   rc=$?
   echo "W=$W rc=$rc $(grep -h '"wall_s"' $OUT/w$W.log | tail -1 | cut -c1-200)"
   [ $rc -ne 0 ] && exit $rc
@@ -19,7 +22,8 @@ done
 python3 - <<'PY'
 import json, glob, os
 rows = []
-for f in sorted(glob.glob("gpurun_out/shards/w*.log"), key=lambda p: int(p.split("w")[-1].split(".")[0])):
+out = os.environ["OUT"]
+for f in sorted(glob.glob(os.path.join(out, "w*.log")), key=lambda p: int(p.split("w")[-1].split(".")[0])):
     W = int(f.split("w")[-1].split(".")[0])
     d = [json.loads(l) for l in open(f) if l.startswith("{") and '"wall_s"' in l][-1]
     rows.append((W, d["sims"], d["wall_s"], d["node_steps_per_s"]))
