@@ -32,6 +32,9 @@ constexpr int kBinsPerThread = (kBins + kThreads - 1) / kThreads;  // 8
 #define WC_WELCH_F64_THREADS 768  // (1024 spills at the 128-VGPR cap; 768: 100 VGPRs, 12 waves)
 #endif
 constexpr int kWelchF64Threads = WC_WELCH_F64_THREADS;
+#ifndef WC_WELCH_W64
+#define WC_WELCH_W64 1  // fp64 rings through welch_wave64_kernel (0: the LDS-Stockham welch_kernel<double>)
+#endif
 
 template <typename R> struct cx { R re, im; };
 template <typename R> __device__ __forceinline__ cx<R> cmul(cx<R> a, cx<R> b) {
@@ -69,8 +72,13 @@ __global__ void twiddle_kernel(double* tw) {
 
 template <typename R>
 __device__ __forceinline__ cx<R> tw_at(const double* tw, int m) {  // exp(-2 pi i m / 4000), m mod 4000
+#if defined(WC_W64_DIAG_NOTW)  // (ablation builds only: timing without the twiddle loads, wrong PSD)
+    (void)tw;
+    return {(R)1 + (R)(m & 1) * (R)1e-30, (R)0};
+#else
     m %= kSeg;
     return {(R)tw[2 * m], (R)tw[2 * m + 1]};
+#endif
 }
 
 // one Stockham stage of radix RAD over the 2000-point FFT, p = product of previous radices
@@ -174,7 +182,11 @@ __global__ void __launch_bounds__(T) welch_kernel(const WelchArgs a) {
                     const int len = (int)min((int64_t)(kSeg - t), a.slot - r);
                     const R* src = col + (q % a.nslots) * a.slot + r;
                     for (int i = tid; i < len; i += T) {
+#if defined(WC_W64_DIAG_NOLOAD)  // (ablation builds only: timing without the segment loads, wrong PSD)
+                        const R v = (R)(i & 7) + (R)(src == nullptr);
+#else
                         const R v = src[i];
+#endif
                         xr[t + i] = v;
                         part[g] += v;
                     }
@@ -244,6 +256,227 @@ __global__ void __launch_bounds__(T) welch_kernel(const WelchArgs a) {
     for (int j = 0; j < kBpt; ++j) {
         const int k = tid + j * T;
         if (k < kBins) a.acc[(int64_t)b * kBins + k] += acc[j];
+    }
+}
+
+// ---------------- fp64 kernel: two waves per column ----------------
+// The reference-precision pipeline's Welch (whole_sweep_both.py:90-95 with the fp64 ring).  The
+// LDS-Stockham welch_kernel<double> above spends most of its time at workgroup barriers and on
+// twiddle loads from memory (20% VALU issue, 58% of wave cycles waiting; profiles/r05/w64_ablation.log).
+// Here a pair of waves (128 threads) owns one column's 2000-point packed FFT in 32 KB of LDS, four
+// columns (eight waves, two per SIMD) per workgroup:
+//   * the 4000-sample segment comes from HBM as 16-B sample pairs, thread t holding packed points
+//     m = t + 128 j (j < 16); the next column's loads are issued as soon as the current one is in
+//     LDS, so they run under its FFT;
+//   * mean (block reduction over the pair) and the periodic Hann window, w(e) = 0.5 - 0.5 Re T^e with
+//     T^(2m) = T^(256 j) T^(2t): the uniform factor an LDS broadcast, the thread's from registers;
+//   * Stockham 2000 = 5 * 5 * 5 * 4 * 4 in place (every read of a stage into registers, a barrier,
+//     every write, a barrier), twiddles from per-stage fp64 tables in LDS (1,995 entries, 31.9 KB);
+//   * the real-FFT unpack with W^k = T^(128 j) T^t, |X_k|^2 summed per thread (bins k = t + 128 j)
+//     over the pair's columns; at the end the four pairs (one simulation per workgroup) are combined
+//     in a fixed order into its fp64 row (single writer, deterministic).
+// Same radix order and butterflies as welch_kernel<double>; the mean and the window are summed /
+// formed in another order (PSD within 1e-12 of it, 1e-9 of the oracle: test_signal_gpu.py).
+constexpr int kW64Cols = 4, kW64Threads = kW64Cols * 128;
+constexpr int kW64Tb2 = 0, kW64Tb3 = kW64Tb2 + 4 * 5, kW64Tb4 = kW64Tb3 + 4 * 25, kW64Tb5 = kW64Tb4 + 3 * 125;
+constexpr int kW64StageTw = kW64Tb5 + 3 * 500;  // 1995
+typedef double d2 __attribute__((ext_vector_type(2)));  // (re, im)
+// LDS: the columns, the stage tables, T^(256 j) and T^(128 j) (j < 16), the pairs' partial sums
+constexpr size_t kW64Lds = ((size_t)kW64Cols * kFFT + kW64StageTw + 32) * sizeof(d2) + kW64Cols * 2 * sizeof(double);
+
+typedef const volatile __attribute__((address_space(3))) d2* lds_d2p;
+__device__ __forceinline__ d2 ldsr64(const d2* p) { return *(lds_d2p)(p); }
+__device__ __forceinline__ d2 cmul64(d2 a, d2 w) {
+    return d2{__builtin_fma(a.x, w.x, -a.y * w.y), __builtin_fma(a.x, w.y, a.y * w.x)};
+}
+
+template <int RAD>
+__device__ __forceinline__ void butterfly64(d2 (&u)[RAD]) {
+    if constexpr (RAD == 4) {
+        const d2 a = u[0] + u[2], b = u[0] - u[2];
+        const d2 c = u[1] + u[3], d = u[1] - u[3];
+        u[0] = a + c;
+        u[2] = a - c;
+        u[1] = d2{b.x + d.y, b.y - d.x};  // b - i d
+        u[3] = d2{b.x - d.y, b.y + d.x};  // b + i d
+    } else {
+        const double c1 = 0.30901699437494742410, c2 = -0.80901699437494742410;  // cos(2pi/5), cos(4pi/5)
+        const double s1 = 0.95105651629515357212, s2 = 0.58778525229247312917;   // sin(2pi/5), sin(4pi/5)
+        const d2 t1 = u[1] + u[4], t2 = u[2] + u[3];
+        const d2 t3 = u[1] - u[4], t4 = u[2] - u[3];
+        const d2 a1 = u[0] + c1 * t1 + c2 * t2;
+        const d2 a2 = u[0] + c2 * t1 + c1 * t2;
+        const d2 b1 = s1 * t3 + s2 * t4, b2 = s2 * t3 - s1 * t4;
+        u[0] = u[0] + t1 + t2;
+        u[1] = d2{a1.x + b1.y, a1.y - b1.x};  // a1 - i b1
+        u[4] = d2{a1.x - b1.y, a1.y + b1.x};
+        u[2] = d2{a2.x + b2.y, a2.y - b2.x};  // a2 - i b2
+        u[3] = d2{a2.x - b2.y, a2.y + b2.x};
+    }
+}
+
+// one radix-RAD Stockham stage over a column's 2000 points, in place (P = product of the previous
+// radices, TB its table base): butterfly i = t + 128 q of the pair's thread t; a partial last row
+// re-reads the stage's last butterfly (clamped) and writes nothing.  Both barriers are workgroup
+// barriers: the four columns of the workgroup step together.
+template <int RAD, int P, int TB>
+__device__ __forceinline__ void w64_stage(d2* z, const d2* Ts, int t) {
+    constexpr int S = kFFT / RAD, NQ = (S + 127) / 128;
+    d2 u[NQ][RAD];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {  // every point read first, back to back
+        const int i = min(t + 128 * q, S - 1);
+#pragma unroll
+        for (int r = 0; r < RAD; ++r) u[q][r] = ldsr64(z + i + r * S);
+    }
+    if constexpr (P > 1) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int k = min(t + 128 * q, S - 1) % P;
+            d2 tw[RAD - 1];  // (plain reads of the read-only table: one LDS wait per row)
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) tw[r - 1] = Ts[TB + (r - 1) * P + k];
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) u[q][r] = cmul64(u[q][r], tw[r - 1]);
+            __builtin_amdgcn_sched_barrier(0);  // one row's twiddles live at a time
+        }
+    }
+    __syncthreads();  // every read of the stage (both waves of the column) before any write
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int i = t + 128 * q, ic = min(i, S - 1), k = ic % P;
+        butterfly64<RAD>(u[q]);
+        if (128 * (q + 1) <= S || i < S) {
+            const int j = (ic - k) * RAD + k;
+#pragma unroll
+            for (int s2i = 0; s2i < RAD; ++s2i) z[j + s2i * P] = u[q][s2i];
+        }
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(kW64Threads, 1) welch_wave64_kernel(const WelchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int c = threadIdx.x >> 7, t = threadIdx.x & 127;  // column slot of the workgroup, thread in the pair
+    const int b = blockIdx.x;
+    d2* z = reinterpret_cast<d2*>(smem) + c * kFFT;
+    d2* Ts = reinterpret_cast<d2*>(smem) + kW64Cols * kFFT;
+    d2* Tj = Ts + kW64StageTw;  // [0, 16): T^(256 j); [16, 32): T^(128 j)
+    double* red = reinterpret_cast<double*>(Tj + 32);  // [column slot][wave of the pair]
+    const d2* T = reinterpret_cast<const d2*>(a.tw);  // T^m = exp(-2 pi i m / 4000), m < 4000
+    // per-stage tables: entry (r - 1) P + k of the stage with (P, RAD) is T^(r k 4000 / (P RAD))
+    for (int e = threadIdx.x; e < kW64StageTw; e += kW64Threads) {
+        int base, P, RAD;
+        if (e < kW64Tb3) { base = kW64Tb2; P = 5; RAD = 5; }
+        else if (e < kW64Tb4) { base = kW64Tb3; P = 25; RAD = 5; }
+        else if (e < kW64Tb5) { base = kW64Tb4; P = 125; RAD = 4; }
+        else { base = kW64Tb5; P = 500; RAD = 4; }
+        const int k = (e - base) % P, r = (e - base) / P + 1;
+        Ts[e] = T[(r * k * (kSeg / (P * RAD))) % kSeg];
+    }
+    if (threadIdx.x < 32) Tj[threadIdx.x] = T[threadIdx.x < 16 ? 256 * threadIdx.x : 128 * (threadIdx.x - 16)];
+    // the thread's factors of the window (T^(2t), T^(2t + 1)) and of the unpack twiddle (T^t)
+    const d2 tl0 = T[2 * t], tl1 = T[2 * t + 1], tu = T[t];
+    const double* E = static_cast<const double*>(a.E);
+    // circular ring per column: sample seg0 + s at (seg0 + s) mod L (byte offsets in 32 bits)
+    const unsigned L = (unsigned)(a.slot * a.nslots);
+    const unsigned baseB = (unsigned)(a.seg0 % L) * 8u, LB = L * 8u;
+    const int64_t bc = (int64_t)b * a.N;
+    double acc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+    d2 x[16];  // samples (2m, 2m + 1) of packed point m = t + 128 j (row 15: threads < 80; others clamp)
+    auto fetch = [&](int n, int tt) {
+        const char* col = reinterpret_cast<const char*>(E + (bc + n) * a.ld);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            unsigned o = baseB + 16u * (unsigned)min(tt + 128 * j, kFFT - 1);
+            o = min(o, o - LB);
+            x[j] = *reinterpret_cast<const d2*>(col + o);
+        }
+    };
+    // every column slot runs the same number of iterations (the stages' workgroup barriers); a slot
+    // past the last column transforms the last one again and adds nothing
+    const int iters = (a.N + kW64Cols - 1) / kW64Cols;
+    fetch(min(c, a.N - 1), t);
+    __syncthreads();  // stage tables in LDS
+    for (int it = 0; it < iters; ++it) {
+        const int n = c + kW64Cols * it;
+        const bool live = n < a.N;
+        // (the thread id laundered per column: hoisted out of the loop, the stages' loop-invariant
+        // twiddle and point addresses would be held across it, i.e. spilled)
+        int tt = t;
+        asm volatile("" : "+v"(tt));
+        tt &= 127;
+        // ---- mean over the 4000 samples (thread partials, each wave, then the pair) ----
+        double sum = 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (j < 15 || tt < 80) sum += x[j].x + x[j].y;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+        if ((tt & 63) == 0) red[c * 2 + (tt >> 6)] = sum;
+        __syncthreads();
+        const double mean = (red[c * 2] + red[c * 2 + 1]) / (double)kSeg;
+        // ---- detrend and window into LDS: w(2m) = 0.5 - 0.5 Re(T^(256 j) T^(2t)) ----
+#pragma unroll
+        for (int jb = 0; jb < 16; jb += 8) {  // (the factors read eight at a time: one LDS wait per batch)
+            d2 tj[8];
+#pragma unroll
+            for (int u8 = 0; u8 < 8; ++u8) tj[u8] = ldsr64(Tj + jb + u8);  // (uniform address: an LDS broadcast)
+#pragma unroll
+            for (int u8 = 0; u8 < 8; ++u8) {
+                const int j = jb + u8;
+                const double c0 = __builtin_fma(tj[u8].x, tl0.x, -tj[u8].y * tl0.y);
+                const double c1 = __builtin_fma(tj[u8].x, tl1.x, -tj[u8].y * tl1.y);
+                const d2 v = d2{__builtin_fma(-0.5, c0, 0.5) * (x[j].x - mean), __builtin_fma(-0.5, c1, 0.5) * (x[j].y - mean)};
+                if (j < 15 || tt < 80) z[tt + 128 * j] = v;
+            }
+        }
+        __syncthreads();
+        // the registers are free: the next column's loads run under this one's FFT
+        if (it + 1 < iters) fetch(min(n + kW64Cols, a.N - 1), tt);
+        w64_stage<5, 1, 0>(z, Ts, tt);
+        w64_stage<5, 5, kW64Tb2>(z, Ts, tt);
+        w64_stage<5, 25, kW64Tb3>(z, Ts, tt);
+        w64_stage<4, 125, kW64Tb4>(z, Ts, tt);
+        w64_stage<4, 500, kW64Tb5>(z, Ts, tt);
+        // ---- unpack X_k = (Z_k + conj Z_{-k})/2 - i/2 W^k (Z_k - conj Z_{-k}), |X_k|^2 ----
+#pragma unroll
+        for (int jb = 0; jb < 16; jb += 4) {  // (four bins read ahead: one LDS wait per batch)
+            d2 Zk4[4], Zc4[4], tj4[4];
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) {
+                const int k = min(tt + 128 * (jb + u4), kFFT);
+                Zk4[u4] = ldsr64(z + (k == kFFT ? 0 : k));
+                Zc4[u4] = ldsr64(z + (k == 0 ? 0 : kFFT - k));
+                tj4[u4] = ldsr64(Tj + 16 + jb + u4);
+            }
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) {
+                const int j = jb + u4;
+                const d2 Zk = Zk4[u4], Zc = Zc4[u4], tj = tj4[u4];
+                const d2 W = d2{__builtin_fma(tj.x, tu.x, -tj.y * tu.y), __builtin_fma(tj.x, tu.y, tj.y * tu.x)};
+                const double er = 0.5 * (Zk.x + Zc.x), ei = 0.5 * (Zk.y - Zc.y);
+                const double dr = Zk.x - Zc.x, di = Zk.y + Zc.y;
+                const double pr = W.x * dr - W.y * di, pi = W.x * di + W.y * dr;
+                const double xr = er + 0.5 * pi, xi = ei - 0.5 * pr;
+                if (live && (j < 15 || tt <= 80)) acc[j] += xr * xr + xi * xi;
+            }
+        }
+        __syncthreads();  // the unpack's reads before the next column's window writes
+    }
+    // ---- the four column slots' sums into the simulation's row (fixed order: single writer) ----
+    double* part = reinterpret_cast<double*>(smem);  // [column slot][16 rows][128 threads]
+#pragma unroll
+    for (int j = 0; j < 16; ++j) part[(c * 16 + j) * 128 + t] = acc[j];
+    __syncthreads();
+    for (int k = threadIdx.x; k < kBins; k += kW64Threads) {
+        const int j = k >> 7, l = k & 127;
+        double s2 = 0.0;
+#pragma unroll
+        for (int v = 0; v < kW64Cols; ++v) s2 += part[(v * 16 + j) * 128 + l];
+        a.acc[(int64_t)b * kBins + k] += s2;
     }
 }
 
@@ -1035,11 +1268,20 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
     hipStream_t st = static_cast<hipStream_t>(stream);
     const bool wave = !e_f64 && ld % 4 == 0 && slot % 4 == 0 && seg0 % 4 == 0 && ((uintptr_t)E & 15) == 0 &&
                       ld < INT32_MAX / 2 - 8192;
+    // fp64 rings: the wave-per-column kernel when sample pairs are 16-B aligned and never split by
+    // the ring's wrap (even seg0, slot * nslots and ld; byte offsets within 32 bits)
+    const bool w64 = WC_WELCH_W64 && e_f64 && seg0 % 2 == 0 && (slot * nslots) % 2 == 0 && ld % 2 == 0 &&
+                     ((uintptr_t)E & 15) == 0 && slot * nslots < INT32_MAX / 8 - 8192;
     // the LDS-Stockham kernels (fp64 input, unaligned rings) take one segment per launch
     for (int sg = 0; sg < (wave ? 1 : nseg); ++sg) {
         WelchArgs a{B, N, E, ld, slot, nslots, seg0 + (int64_t)sg * (kSeg / 2), wave ? nseg : 1,
                     static_cast<const double*>(workspace), acc};
-        if (e_f64) {
+        if (e_f64 && w64) {
+            hipError_t ea = hipFuncSetAttribute((const void*)welch_wave64_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kW64Lds);
+            if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
+            hipLaunchKernelGGL(welch_wave64_kernel, dim3(B), dim3(kW64Threads), kW64Lds, st, a);
+        } else if (e_f64) {
             constexpr int T = kWelchF64Threads;
             const size_t lds = (size_t)2 * kG<double> * kFFT * sizeof(cx<double>) + (T / 64) * kG<double> * sizeof(double);
             hipError_t ea = hipFuncSetAttribute((const void*)welch_kernel<double, T>,

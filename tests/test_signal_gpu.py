@@ -201,6 +201,39 @@ def test_welch_f32_two_segments_per_launch(cuda, B, N, K):
         np.testing.assert_allclose(psd2[b].cpu().numpy(), mp, rtol=2e-4, atol=2e-4 * mp.max())
 
 
+@pytest.mark.parametrize("B,N", [(5, 1), (2, 3), (4, 9), (2, 90)])
+def test_welch_f64_wave_kernel_ring_wrap(cuda, B, N):
+    """fp64 rings: the wave-per-column kernel (even ld, slot, seg0) reading a segment that wraps
+    the 4-slot ring against the LDS-Stockham welch_kernel<double> (an odd ld selects it) on the same
+    samples: the same PSD to 1e-12 (the mean and the window are formed in another order), the same
+    peaks; and the oracle's PSD within 1e-9.  N < 4 leaves waves of the workgroup idle."""
+    T = 6000
+    X = torch.from_numpy(_e_like(T, B * N, B * 30 + N).T.copy()).to("cuda", torch.float64)  # [C][T]
+    slot, nslots, ld = 1000, 4, 4096
+    ring = torch.zeros((B * N, ld), dtype=torch.float64, device="cuda")
+    for t0 in range(2000, T, slot):  # samples [2000, 6000) into slots (t // slot) % 4
+        q = (t0 // slot) % nslots
+        ring[:, q * slot:(q + 1) * slot] = X[:, t0:t0 + slot]
+    a = wsg.WelchAccumulator(B, N)
+    a.accumulate(ring.reshape(-1), ld, slot, nslots, 2000)  # runs: slots 2, 3, 0, 1
+    odd = torch.zeros((B * N, 4001), dtype=torch.float64, device="cuda")
+    odd[:, :4000] = X[:, 2000:]
+    c = wsg.WelchAccumulator(B, N)
+    c.accumulate(odd.reshape(-1), 4001, 4000, 1, 0)  # odd ld: welch_kernel<double>
+    pa, psd = a.peak(want_psd=True)
+    pc, _ = c.peak(want_psd=True)
+    torch.cuda.synchronize()
+    rel = ((a.acc - c.acc).abs().max() / c.acc.abs().max()).item()
+    print(f"TOL welch-f64-wave-vs-lds-{B}-{N} rel={rel:.3e}")
+    assert rel <= 1e-12
+    assert torch.equal(pa, pc)
+    Xh = X.cpu().numpy().reshape(B, N, T)
+    for b in range(B):
+        f, P = osg.welch_psd(Xh[b][:, 2000:], 500.0, 4000)
+        mp = P.mean(axis=0)
+        np.testing.assert_allclose(psd[b].cpu().numpy(), mp, rtol=1e-9, atol=1e-9 * mp.max())
+
+
 def test_welch_golden_full_length(cuda):
     """300,000-sample input of the SciPy golden: node-mean PSD and peak."""
     inp = inputs()
