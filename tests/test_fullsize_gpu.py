@@ -66,3 +66,23 @@ def test_full_pipeline_shard_invariance(cuda, sc90):
     for k, v in part.columns().items():
         assert np.array_equal(v, full.columns()[k][shard]), k
     assert np.isfinite(full.metrics).all() and (full.peakfreq > 0).all()
+
+
+def test_f64_full_batch_tail_launch_invariance(cuda, sc90):
+    """The fp64 integrator at the full batch runs two launches (the two-group rounds over the first
+    2 x 256 x 2 groups of 16, then one-group workgroups for the rest, wc_sde.hip launch_f64_nt6):
+    a simulation gives the same bits wherever it sits -- in a small batch (one-group workgroups
+    only), in the main launch or in the tail one of the full batch."""
+    G, S, keys = sweep_batch(0)
+    B = len(keys)
+    p = driver_params()
+    full = Batch(sc90, G, S, keys, p, precision="f64")
+    full.integrate(40, 0.05)
+    full.integrate(40, 2.0)
+    ref = _state(full)
+    # sims from the main launch's first and last groups and from the tail
+    pick = np.r_[0:16, 16 * 1023:16 * 1025, B - 40:B]
+    sb = Batch(sc90, G[pick], S[pick], keys[pick], p, precision="f64")
+    sb.integrate(40, 0.05)
+    sb.integrate(40, 2.0)
+    assert np.array_equal(_state(sb), ref[:, pick])
