@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""consumer_golden.npz: the reference's OWN consumers run on this build's outputs (build container only).
+
+SURVEY.md 8(f) rank 2: heatmaps.py and the pickle loaders of analyze_many_seeds.py / Fig5 must run
+unchanged on what the sweep drivers write.  Those scripts cannot be imported here (seaborn,
+matplotlib, statsmodels and data paths at module top level), but the consumer functions themselves
+need only numpy and pandas.  This generator reads the reference sources at generation time, takes
+out with `ast` exactly
+
+  * heatmaps.py:30-72          ``extract(filepath, ...)`` plus the module constants it closes over
+                               (``states``, ``var_ex``, ``thx``, ``thy``, heatmaps.py:22-28),
+  * analyze_many_seeds.py:69-81 ``load(dic)``          (+ ``states``, :19),
+  * figures/Fig5/fig5.py:117-129 ``load(dic, nseeds=50)`` (+ ``states``, :24),
+
+executes those definitions unmodified in a namespace holding numpy and pandas, and applies them to
+
+  (i)  the reference's shipped homogeneous table (output/sweep_delta_homoW_..._9dic24_50iter.txt),
+       committed gz'd as tests/golden/shipped_homo_table.csv.gz so the CPU test has the same input;
+  (ii) this build's full C3 sweep table (profiles/r06_homo_sweep.txt.gz: 20,000 simulations x the
+       full 1001 s schedule, written by `python -m nremmodfc_amd.sweep homo` on one MI355X);
+  (iii) this build's C2 pickle (`python -m nremmodfc_amd.sweep many --modality homo`, 200
+       simulations with device HMA; our own file, loaded with pickle).
+
+Only OUTPUTS are committed (plot matrices, optima, violins; matts, Hin_nodes, Hse_nodes) together
+with the sha256 of each input, so tests/test_consumers.py can show that its restatement of these
+functions equals the reference's code on the same inputs, and the -m gpu C2 test can show that
+the engine regenerates the pickle's contents exactly.  No reference source is copied.
+
+  python tests/golden/make_consumer_golden.py --pickle gpurun_out/r06a/many/run_50seeds_output_homo.pickle
+"""
+import argparse
+import ast
+import gzip
+import hashlib
+import os
+import pickle
+import shutil
+import sys
+import warnings
+
+import numpy as np
+import pandas as pd
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+SHIPPED_HOMO = os.path.join(REF, "output", "sweep_delta_homoW_fromG0.16_sigma7.68_maps_0_0_9dic24_50iter.txt")
+SHIPPED_COPY = os.path.join(HERE, "shipped_homo_table.csv.gz")
+PRODUCT_TABLE = os.path.join(ROOT, "profiles", "r06_homo_sweep.txt.gz")
+STATES = ("W", "N1", "N2", "N3")
+
+
+def reference_defs(relpath, funcs, consts):
+    """The named top-level functions and the FIRST top-level assignment of each named constant of
+    a reference source file, executed (unchanged) in a fresh namespace with np and pd."""
+    src = open(os.path.join(REF, relpath)).read()
+    tree = ast.parse(src)
+    keep, seen = [], set()
+    for node in tree.body:
+        if isinstance(node, ast.FunctionDef) and node.name in funcs:
+            keep.append(node)
+        elif isinstance(node, ast.Assign) and len(node.targets) == 1 and isinstance(node.targets[0], ast.Name):
+            name = node.targets[0].id
+            if name in consts and name not in seen:
+                seen.add(name)
+                keep.append(node)
+    missing = (set(funcs) | set(consts)) - {getattr(n, "name", None) for n in keep} - seen
+    assert not missing, (relpath, missing)
+    ns = {"np": np, "pd": pd, "__name__": "ref_" + os.path.basename(relpath)[:-3]}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), os.path.join(REF, relpath), "exec"), ns)
+    return ns
+
+
+def sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
+def pickle_digest(d):
+    """sha256 over the pickle's contents in a fixed order (key order, then each array's bytes):
+    independent of how the dict was pickled."""
+    h = hashlib.sha256()
+    h.update(repr(sorted((k, v) for k, v in d["metainfo"].items())).encode())
+    for key in sorted(k for k in d if k != "metainfo"):
+        h.update(repr(key).encode())
+        v = d[key]
+        for name in ("Hin_sim", "Hse_sim", "Hin_node_sim", "Hse_node_sim", "sFC"):
+            h.update(name.encode())
+            h.update(np.ascontiguousarray(np.asarray(v[name], dtype=np.float64)).tobytes())
+    return h.hexdigest()
+
+
+def heatmap_fields(prefix, out):
+    return {f"{prefix}__x_vals": out["x_vals"], f"{prefix}__y_vals": out["y_vals"],
+            f"{prefix}__plotmats": np.stack(out["plotmats"]), f"{prefix}__coors_o": np.array(out["coors_o"]),
+            f"{prefix}__vals_o": np.array(out["vals_o"]), f"{prefix}__violins_o": np.stack(out["violins_o"])}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pickle", required=True, help="the C2 pickle written by `sweep many --modality homo`")
+    args = ap.parse_args()
+    warnings.filterwarnings("ignore")  # heatmaps.py:18-19 does the same (pandas chained-assignment notes)
+
+    hm = reference_defs("heatmaps.py", ["extract"], ["states", "var_ex", "thx", "thy"])
+    asm = reference_defs("analyze_many_seeds.py", ["load"], ["states"])
+    f5 = reference_defs(os.path.join("figures", "Fig5", "fig5.py"), ["load"], ["states"])
+
+    if not os.path.exists(SHIPPED_COPY) or pd.read_csv(SHIPPED_COPY).shape != pd.read_csv(SHIPPED_HOMO).shape:
+        with open(SHIPPED_HOMO, "rb") as fi, gzip.GzipFile(SHIPPED_COPY, "wb", mtime=0) as fo:
+            shutil.copyfileobj(fi, fo)
+    assert pd.read_csv(SHIPPED_COPY).equals(pd.read_csv(SHIPPED_HOMO))
+
+    out = {}
+    # extract() reads the file itself (pd.read_csv(filepath), heatmaps.py:31): give it the paths
+    for prefix, path in (("shipped_homo", SHIPPED_COPY), ("product_homo", PRODUCT_TABLE)):
+        res = hm["extract"](path)
+        out.update(heatmap_fields(prefix, res))
+        out[f"{prefix}__sha256"] = np.array(sha256(path))
+        print(prefix, [tuple(np.round(v, 4)) for v in res["vals_o"][:4]])
+
+    with open(args.pickle, "rb") as f:  # our own file (written by nremmodfc_amd.sweep)
+        d = pickle.load(f)
+    out["c2_homo__digest"] = np.array(pickle_digest(d))
+    for tag, ns in (("asm", asm), ("fig5", f5)):
+        matts, hin, hse = ns["load"]({k: dict(v) if k != "metainfo" else v for k, v in d.items()})
+        out[f"c2_homo__{tag}_matts"] = np.stack([matts[s] for s in STATES])
+        out[f"c2_homo__{tag}_Hin_nodes"] = np.stack([hin[s] for s in STATES])
+        out[f"c2_homo__{tag}_Hse_nodes"] = np.stack([hse[s] for s in STATES])
+    np.savez_compressed(os.path.join(HERE, "consumer_golden.npz"), **out)
+    print("c2 digest", out["c2_homo__digest"])
+
+
+if __name__ == "__main__":
+    main()

@@ -1,27 +1,39 @@
-"""The reference's own consumer of the sweep table, heatmaps.py, on this build's output.
+"""The reference's own consumers of the sweep outputs, on this build's outputs.
 
-heatmaps.py cannot be imported here (seaborn, matplotlib at module top), so its extract()
-(heatmaps.py:30-72) is restated line for line below, without the plotting; the restatement
-reproduces the optima run_many_seeds.py:34-38 quotes for the homogeneous model when applied to
-the shipped table (tests/golden/shipped_heatmaps.npz, made by make_heatmap_golden.py).
+heatmaps.py, analyze_many_seeds.py and figures/Fig5/fig5.py cannot be imported here (seaborn,
+matplotlib, statsmodels and data paths at module top level), and /root/reference does not travel
+to the GPU box.  tests/golden/make_consumer_golden.py therefore ran the REFERENCE's own functions --
+heatmaps.py:30-72 ``extract`` and the pickle loaders analyze_many_seeds.py:69-81 / fig5.py:117-129
+``load``, taken out of the sources with ``ast`` and executed unmodified -- on
 
-Applied to this build's full homogeneous sweep (profiles/r02_homo_sweep.txt.gz: 20,000
-simulations x 1001 s, read with pandas exactly as heatmaps.py reads output/*.txt) it must give
-euccorr maps that track the shipped ones cell by cell, and the same W optimum.
+  * the shipped homogeneous table (tests/golden/shipped_homo_table.csv.gz),
+  * this build's full C3 sweep (profiles/r06_homo_sweep.txt.gz: 20,000 simulations x 1001 s on one
+    MI355X, `python -m nremmodfc_amd.sweep homo`),
+  * this build's C2 pickle (`sweep many --modality homo`, 200 simulations, device HMA),
+
+and committed their outputs (tests/golden/consumer_golden.npz).  The restatements below must give
+those outputs EXACTLY on the same inputs; the -m gpu test regenerates the C2 pickle with the engine
+(deterministic) and checks its contents against the digest of the one the reference's loaders read.
 """
 import os
 
 import numpy as np
 import pandas as pd
+import pytest
+
+from tests.golden.make_consumer_golden import pickle_digest, sha256
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden", "consumer_golden.npz")
+SHIPPED = os.path.join(ROOT, "tests", "golden", "shipped_homo_table.csv.gz")
+PRODUCT = os.path.join(ROOT, "profiles", "r06_homo_sweep.txt.gz")
 STATES = ("W", "N1", "N2", "N3")
 VAR_EX = {"euccorr": "min", "e": "min", "ssim": "max", "corr": "max"}  # heatmaps.py:23
-THX, THY = (-0.08, 0.2), (-0.2, 0.08)                                  # heatmaps.py:26
+THX, THY = (-0.08, 0.2), (-0.2, 0.08)                                  # heatmaps.py:28
 
 
 def extract(data_pre, xv="delta_G", yv="delta_sigma", var2see="euccorr", C1=0, w=1, thx=THX, thy=THY):
-    """heatmaps.py:30-72 without the violin padding's plotting use; returns the same dict."""
+    """heatmaps.py:30-72 restated (takes the DataFrame instead of the path); the same dict."""
     nseed = 50
     data_pre = data_pre[(thx[0] <= data_pre[xv]) & (data_pre[xv] <= thx[1]) & (thy[0] <= data_pre[yv])
                         & (data_pre[yv] <= thy[1])].copy()
@@ -50,27 +62,81 @@ def extract(data_pre, xv="delta_G", yv="delta_sigma", var2see="euccorr", C1=0, w
             "violins_o": violins_o}
 
 
-def test_restated_consumer_gives_the_reference_optima():
-    g = np.load(os.path.join(ROOT, "tests", "golden", "shipped_heatmaps.npz"))
-    # run_many_seeds.py:34-38, homogeneous: W (0, 0), N1 (0.04, 0), N2 (0, 0), N3 (-0.04, 0.04)
+def load_many_seeds(dic, nseeds=None):
+    """analyze_many_seeds.py:69-81 (nseeds from "metainfo") / fig5.py:117-129 (nseeds=50) restated:
+    per-state seed-mean FC, and the per-seed nodal integration / segregation."""
+    n = {st: (dic["metainfo"][st] if nseeds is None else nseeds) for st in STATES}
+    matts = {st: np.zeros((n[st], 90, 90)) for st in STATES}
+    hin = {st: np.zeros((n[st], 90)) for st in STATES}
+    hse = {st: np.zeros((n[st], 90)) for st in STATES}
+    for key, v in dic.items():
+        if key != "metainfo":
+            s, state = key
+            matts[state][s] = v["sFC"]
+            hin[state][s] = v["Hin_node_sim"]
+            hse[state][s] = v["Hse_node_sim"]
+    return {st: matts[st].mean(axis=0) for st in STATES}, hin, hse
+
+
+def _check_extract_equals_reference(path, prefix):
+    g = np.load(GOLD)
+    assert sha256(path) == str(g[f"{prefix}__sha256"]), f"{path} is not the input the reference's extract() read"
+    ours = extract(pd.read_csv(path))
+    np.testing.assert_array_equal(ours["x_vals"], g[f"{prefix}__x_vals"])
+    np.testing.assert_array_equal(ours["y_vals"], g[f"{prefix}__y_vals"])
+    np.testing.assert_array_equal(np.stack(ours["plotmats"]), g[f"{prefix}__plotmats"])
+    np.testing.assert_array_equal(np.array(ours["coors_o"]), g[f"{prefix}__coors_o"])
+    np.testing.assert_array_equal(np.array(ours["vals_o"]), g[f"{prefix}__vals_o"])
+    np.testing.assert_array_equal(np.stack(ours["violins_o"]), g[f"{prefix}__violins_o"])
+    return ours
+
+
+def test_restated_extract_equals_reference_on_shipped_table():
+    ours = _check_extract_equals_reference(SHIPPED, "shipped_homo")
+    # and the reference's own code gives the optima run_many_seeds.py:34-38 quotes for the
+    # homogeneous model: W (0, 0), N1 (0.04, 0), N2 (0, 0), N3 (-0.04, 0.04)
     want = [(0.0, 0.0), (0.04, 0.0), (0.0, 0.0), (-0.04, 0.04)]
-    assert [tuple(np.round(v[:2], 4)) for v in g["vals_o"][:4]] == want
+    assert [tuple(np.round(v[:2], 4)) for v in ours["vals_o"][:4]] == want
 
 
-def test_heatmaps_on_this_builds_full_sweep():
-    ours = extract(pd.read_csv(os.path.join(ROOT, "profiles", "r02_homo_sweep.txt.gz")))
-    g = np.load(os.path.join(ROOT, "tests", "golden", "shipped_heatmaps.npz"))
-    np.testing.assert_allclose(ours["x_vals"], g["x_vals"])
-    np.testing.assert_allclose(ours["y_vals"], g["y_vals"])
+def test_restated_extract_equals_reference_on_this_builds_sweep():
+    _check_extract_equals_reference(PRODUCT, "product_homo")
+
+
+def test_heatmaps_of_this_builds_sweep_track_the_shipped_ones():
+    """The reference's extract() output on the build's table against its output on the shipped
+    table (both from consumer_golden.npz): the same axes, cell maps correlated > 0.99, the same W
+    optimum; the sleep states' optima lie on a flat valley (within 5% of the shipped optimum's value)."""
+    g = np.load(GOLD)
+    np.testing.assert_array_equal(g["product_homo__x_vals"], g["shipped_homo__x_vals"])
+    np.testing.assert_array_equal(g["product_homo__y_vals"], g["shipped_homo__y_vals"])
     for k, st in enumerate(STATES + ("mean", "sync", "meta")):
-        a, b = g["plotmats"][k], ours["plotmats"][k]
+        a, b = g["shipped_homo__plotmats"][k], g["product_homo__plotmats"][k]
         r = np.corrcoef(a.ravel(), b.ravel())[0, 1]
         rel = np.abs(b - a).max() / np.abs(a).max()
         print(f"{st}: cell maps r = {r:.4f}, max relative cell difference {rel:.3f}")
         assert r > 0.99 and rel < 0.08, (st, r, rel)
-    assert tuple(np.round(ours["vals_o"][0][:2], 4)) == (0.0, 0.0)  # the W optimum of the model
-    # the other states' optima sit on a flat valley: each of ours is within 0.05 of the shipped
-    # one's euccorr value at the shipped optimum
+    ours, ship = g["product_homo__vals_o"], g["shipped_homo__vals_o"]
+    assert tuple(np.round(ours[0][:2], 4)) == (0.0, 0.0)
     for k in range(1, 4):
-        xo, yo, oval = g["vals_o"][k]
-        assert ours["vals_o"][k][2] <= oval * 1.05
+        assert ours[k][2] <= ship[k][2] * 1.05
+
+
+@pytest.mark.gpu
+def test_c2_pickle_regenerates_and_loads_like_the_reference(tmp_path, cuda):
+    """run_many_seeds.py (C2, homogeneous optima) through the product on this GPU: the pickle's
+    contents equal the pickle the reference's loaders read when the fixture was made (sha256 of
+    every array), and the restated loaders give the reference's matts / Hin_nodes / Hse_nodes."""
+    import pickle
+    from nremmodfc_amd import sweep
+    out = str(tmp_path)
+    sweep.main(["many", "--modality", "homo", "--out", out, "--tag", "c2h"])
+    with open(os.path.join(out, "c2h.pickle"), "rb") as f:  # our own file
+        d = pickle.load(f)
+    g = np.load(GOLD)
+    assert pickle_digest(d) == str(g["c2_homo__digest"])
+    for tag, nseeds in (("asm", None), ("fig5", 50)):
+        matts, hin, hse = load_many_seeds(d, nseeds)
+        np.testing.assert_array_equal(np.stack([matts[s] for s in STATES]), g[f"c2_homo__{tag}_matts"])
+        np.testing.assert_array_equal(np.stack([hin[s] for s in STATES]), g[f"c2_homo__{tag}_Hin_nodes"])
+        np.testing.assert_array_equal(np.stack([hse[s] for s in STATES]), g[f"c2_homo__{tag}_Hse_nodes"])

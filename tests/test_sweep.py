@@ -370,16 +370,12 @@ def test_many_seeds_full_size(tmp_path, cuda):
     with open(os.path.join(out, "c2.pickle"), "rb") as f:  # our own file
         d = pickle.load(f)
     assert d["metainfo"] == {s: 50 for s in datasets.STATES}
-    matts = {st: np.zeros((50, 90, 90)) for st in datasets.STATES}
-    hin = {st: np.zeros((50, 90)) for st in datasets.STATES}
-    hse = {st: np.zeros((50, 90)) for st in datasets.STATES}
+    from tests.test_consumers import load_many_seeds  # fig5.py:117-129's load(dic, nseeds=50)
+    matts, hin, hse = load_many_seeds(d, 50)
     for key in d:
         if key != "metainfo":
-            s, state = key
-            matts[state][s] = d[key]["sFC"]
-            hin[state][s] = d[key]["Hin_node_sim"]
-            hse[state][s] = d[key]["Hse_node_sim"]
             assert np.isscalar(d[key]["Hin_sim"]) or np.ndim(d[key]["Hin_sim"]) == 0
+    matts = {st: np.stack([d[(s, st)]["sFC"] for s in range(50)]) for st in datasets.STATES}
     for st in datasets.STATES:
         assert np.isfinite(matts[st]).all() and (matts[st] >= 0).all()
         assert np.isfinite(hin[st]).all() and np.isfinite(hse[st]).all()

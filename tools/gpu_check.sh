@@ -2,19 +2,20 @@
 # One GPU session: parity tests, smoke, short bench, rocprof kernel trace; optionally the
 # reference-precision bench (bench64), the full homogeneous sweep with its statistics against the
 # shipped table (sweep) and the CPU baseline against core count (cpu).
-#   STEPS="tests smoke bench prof bench64 sweep cpu" bash tools/gpu_check.sh
+#   STEPS="tests smoke bench prof bench64 sweep many cpu" bash tools/gpu_check.sh
+# OUT (default gpurun_out) names the output directory; TESTS selects the pytest targets.
 # Stops at the first crash/timeout (exit codes other than 0/1 from pytest).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out
+OUT=${OUT:-gpurun_out}
 mkdir -p $OUT
 STEPS="${STEPS:-tests smoke bench prof}"
 fatal() { local rc=$1; [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; }
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -rA --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
       echo "pytest gpu rc=$rc"; tail -25 $OUT/pytest_gpu.log
       if fatal $rc; then echo "STOP after tests"; exit $rc; fi ;;
     smoke)
@@ -41,6 +42,11 @@ for s in $STEPS; do
       f=$(ls $OUT/homo/*.txt | head -1)
       timeout -k 10 300 python tools/validate_stats.py "$f" homo $OUT/homo_stats.json > $OUT/homo_val.log 2>&1 || { echo "validate failed"; tail -5 $OUT/homo_val.log; exit 1; }
       tail -16 $OUT/homo_val.log ;;
+    many)
+      # run_many_seeds.py (C2): 50 seeds x 4 states with device HMA -> the pickle the consumers read
+      timeout -k 10 300 python -m nremmodfc_amd.sweep many --modality ${MODALITY:-homo} --out $OUT/many > $OUT/many.log 2>&1; rc=$?
+      echo "many rc=$rc"; tail -1 $OUT/many.log | cut -c1-300
+      if [ $rc -ne 0 ]; then echo "STOP after many"; exit $rc; fi ;;
     cpu)
       timeout -k 10 300 python -u tools/cpu_scaling.py > $OUT/cpu_scaling.log 2>&1; rc=$?
       echo "cpu rc=$rc"; cat $OUT/cpu_scaling.log
