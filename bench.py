@@ -41,6 +41,7 @@ PEAK_FP64_TFLOPS = 78.6
 PEAK_HBM_GBPS = 8000.0     # MI355X HBM3E (MI355X_MICROARCH.md)
 PEAK_F16_TFLOPS = 2500.0   # dense fp16 MFMA (MI355X_MICROARCH.md); the fp16x3 coupling runs on it
 PEAK_IC_GATHER_GBPS = 8600.0  # rows gathered from the Infinity Cache into the CUs, chip-wide (MI355X_MICROARCH.md)
+PEAK_L2_GATHER_GBPS = 18800.0  # L2-resident rows gathered into the CUs, chip-wide (the guide's 16.8-18.8 TB/s)
 
 
 def flops_per_node_step(N):
@@ -147,7 +148,7 @@ def cpu_baseline_compiled(sc, seconds=8.0, steps=2000):
                     "cores_available); profiles/r04_cpu_scaling.log has the per-core rate at 1..16 cores"}
 
 
-def cpu_baseline(sc, seconds=8.0, steps=2000):
+def cpu_baseline(sc, seconds=8.0, steps=2000, numpy_leg=True):
     """N = 90: the reported baseline is the compiled port (oracle/wc_oracle.c): the reference
     decorates run() and wilsonCowan with numba's @njit (netwWilsonCowanPlastic.py:77,86) and cannot
     be imported without numba, so as shipped its loop always runs compiled.  The interpreted NumPy
@@ -160,8 +161,9 @@ def cpu_baseline(sc, seconds=8.0, steps=2000):
     N = sc.shape[0]
     if N == 90:
         out = cpu_baseline_compiled(sc, seconds, steps)
-        out["numpy_interpreted"] = cpu_baseline_numpy(steps=max(2000, int(seconds * 20_000)))
-        out["numpy_interpreted"]["kind"] = "interpreted"
+        if numpy_leg:
+            out["numpy_interpreted"] = cpu_baseline_numpy(steps=max(2000, int(seconds * 20_000)))
+            out["numpy_interpreted"]["kind"] = "interpreted"
         return out
     comp = cpu_baseline_compiled(sc, seconds, steps=max(20, int(steps * (90 / N) ** 2)))
     nump = cpu_baseline_numpy(steps=max(200, int(seconds * 2_000_000 / N)), nodes=N)
@@ -276,44 +278,9 @@ def run_workload(sc, G, S, keys, p, args, dev, dist, steps, warmup):
     return elapsed, kern
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--precision", default="f32", choices=("f32", "f64"))
-    ap.add_argument("--config", default="c3", choices=("c3", "c5"),
-                    help="c3: 20,000 sims x 90 nodes per GPU (the metric's config); c5: the 1000-node "
-                         "synthetic connectome, 2,500 sims per GPU (20,000 over 8 GPUs)")
-    ap.add_argument("--sde-only", action="store_true",
-                    help="time the integrator alone (no streamed BOLD / Welch consumers)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
-                    help="nccl (RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0)
-    ap.add_argument("--scaling", default=None, choices=("weak", "strong"),
-                    help="strong (the c3 default): the one c3 sweep (20,000 sims) or c5 sweep (20,000 sims over 8 "
-                         "GPUs = 2,500 x 8) split round-robin over the ranks; weak (the c5 default): 20,000 (c3) / "
-                         "2,500 (c5) sims per rank")
-    ap.add_argument("--weak-steps", type=int, default=2,
-                    help="c3, strong, N > 1: also time this many steps of the weak-scaling job (every rank its "
-                         "own 20,000-sim sweep) and report its aggregate as weak_scaling (0: skip)")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.dist_backend == "gloo":  # rehearsal: ranks may share a device
-        local %= torch.cuda.device_count()
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
-
+def measure(args, world, rank, local, dist, cpu_seconds=None, cpu_numpy=True):
+    """One bench line for args.config / args.precision: time the workload, attach the roofline, and
+    (rank 0 of a one-GPU run, cpu_seconds given) the CPU baseline of the same workload."""
     if args.scaling is None:  # c3: the ONE sweep north_star names, split over the ranks (identical at N = 1)
         args.scaling = "strong" if args.config == "c3" else "weak"
     if args.scaling == "strong":  # one sweep, the reference's round robin (whole_sweep_both.py:63-64)
@@ -451,6 +418,19 @@ def main():
         res_k = min(Np // 32, 8) * 32  # K columns of each connectome tile kept in LDS (kPRes chunks of 32)
         # operand bytes per step: the streamed part of the A rows + the E image, per workgroup
         stream = (Np // 128) * (Bp // 80) * (128 * (Np - res_k) + 80 * Np) * 4
+        gbps = stream * EULER / t_launch / 1e9
+        opnd = {"bytes_per_step": stream, "GBps": gbps, "ic_gather_peak_GBps": PEAK_IC_GATHER_GBPS,
+                "x_ic_gather_peak": gbps / PEAK_IC_GATHER_GBPS,
+                "peak_note": "MI355X_MICROARCH.md 'Indexed rows: gather into LDS': rows from the Infinity Cache "
+                             "8.6 TB/s chip-wide, L2-resident rows 16.8-18.8 TB/s"}
+        tcc = stamped(os.path.join(ROOT, "profiles", "pmc_c5_tcc.json"))
+        if tcc.get("l2_hit_rate") is not None and tcc.get("kernel") == pmc_d.get("kernel"):
+            # the requests the L2 serves at the L2-resident rate, the rest at the Infinity-Cache rate
+            h = tcc["l2_hit_rate"]
+            ceil = 1.0 / (h / PEAK_L2_GATHER_GBPS + (1 - h) / PEAK_IC_GATHER_GBPS)
+            opnd.update({"l2_hit_rate": h, "split_peak_GBps": ceil, "frac": gbps / ceil,
+                         "model": "ceiling = 1 / (h / 18.8 TB/s + (1 - h) / 8.6 TB/s), h = PMC L2 hit rate "
+                                  "(profiles/pmc_c5_tcc.json, stamped on this library)"})
         roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / PEAK_F16_TFLOPS, "traffic": traffic,
                 "traffic_algorithmic": per_launch_ns * 24,
@@ -459,19 +439,13 @@ def main():
                 "algorithmic_flops_per_node_step": fl,
                 "issued_f16_flops_per_node_step": ifl,
                 "algorithmic_tflops_fp32_equiv": per_launch_ns * fl / t_launch / 1e12,
-                "operand_stream": {"bytes_per_step": stream,
-                                   "GBps": stream * EULER / t_launch / 1e9,
-                                   "peak_GBps": PEAK_IC_GATHER_GBPS,
-                                   "frac": stream * EULER / t_launch / 1e9 / PEAK_IC_GATHER_GBPS,
-                                   "peak_note": "MI355X_MICROARCH.md 'Indexed rows: gather into LDS': rows of a "
-                                                "38 MB table from the Infinity Cache, 8.6 TB/s chip-wide (L2-resident "
-                                                "rows 16.8-18.8 TB/s)"},
-                "binding": "operand_stream",
-                "note": "fp16 MFMA roofline of the issued coupling work (frac); the kernel is bound by the per-step "
-                        "operand stream from L2/Infinity Cache, priced in operand_stream.frac against the Infinity-Cache "
-                        "row-gather rate (ablation without the K-loop loads: 14.8 of 24.2 us per step). "
-                        "traffic = PMC FETCH+WRITE per launch; traffic_algorithmic = 24 B per node-step of "
-                        "state streaming, which this kernel no longer moves"}
+                "operand_stream": opnd,
+                "note": "frac = the issued fp16x3 coupling flops (padding included) over the dense fp16 MFMA peak. "
+                        "operand_stream prices the per-step operand bytes (streamed connectome rows + E image) "
+                        "against the L2-hit / Infinity-Cache-miss split of the gather rates; neither ceiling is "
+                        "reached: the step is latency-bound (DESIGN.md 3.1b). traffic = PMC FETCH+WRITE per "
+                        "launch; traffic_algorithmic = 24 B per node-step of state streaming, which this kernel "
+                        "does not move"}
     roof["kernel_ms_per_launch"] = kern["sde"]
     roof["pmc"] = util or None
     roof["pmc_lib_sha256"] = stamp if pmc_d else None
@@ -508,10 +482,70 @@ def main():
         "kernel_ms": kern,
         "weak_scaling": weak,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(sc, seconds=args.cpu_seconds)
-    elif rank == 0:
+    if rank == 0 and world == 1 and cpu_seconds:
+        out["cpu_baseline"] = cpu_baseline(sc, seconds=cpu_seconds, numpy_leg=cpu_numpy)
+    else:
         out["cpu_baseline"] = None
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--precision", default="f32", choices=("f32", "f64"))
+    ap.add_argument("--config", default="c3", choices=("c3", "c5"),
+                    help="c3: 20,000 sims x 90 nodes per GPU (the metric's config); c5: the 1000-node "
+                         "synthetic connectome, 2,500 sims per GPU (20,000 over 8 GPUs)")
+    ap.add_argument("--sde-only", action="store_true",
+                    help="time the integrator alone (no streamed BOLD / Welch consumers)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--scaling", default=None, choices=("weak", "strong"),
+                    help="strong (the c3 default): the one c3 sweep (20,000 sims) or c5 sweep (20,000 sims over 8 "
+                         "GPUs = 2,500 x 8) split round-robin over the ranks; weak (the c5 default): 20,000 (c3) / "
+                         "2,500 (c5) sims per rank")
+    ap.add_argument("--secondary-steps", type=int, default=2,
+                    help="the default c3 f32 line also times the C5 (1000-node) and the fp64 (reference precision) "
+                         "workloads for this many steps each, reported under `secondary` (0: skip)")
+    ap.add_argument("--weak-steps", type=int, default=2,
+                    help="c3, strong, N > 1: also time this many steps of the weak-scaling job (every rank its "
+                         "own 20,000-sim sweep) and report its aggregate as weak_scaling (0: skip)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend == "gloo":  # rehearsal: ranks may share a device
+        local %= torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+
+    out = measure(args, world, rank, local, dist, None if args.no_cpu_baseline else args.cpu_seconds)
+    if args.config == "c3" and args.precision == "f32" and not args.sde_only and args.secondary_steps > 0:
+        # north_star asks for the 1000-node throughput and the reference-precision line beside the
+        # headline: both timed in the same run, each with its own roofline, kernel times and CPU baseline
+        sec = {}
+        for name, cfg, prec in (("c5", "c5", "f32"), ("f64", "c3", "f64")):
+            a2 = argparse.Namespace(**vars(args))
+            a2.config, a2.precision, a2.scaling, a2.weak_steps = cfg, prec, None, 0
+            a2.steps, a2.warmup = args.secondary_steps, 1
+            torch.cuda.empty_cache()
+            r = measure(a2, world, rank, local, dist,
+                        None if args.no_cpu_baseline else args.cpu_seconds / 2, cpu_numpy=(cfg == "c5"))
+            sec[name] = {k: r[k] for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "scaling",
+                                           "dtype", "dtype_detail", "data", "config", "roofline", "kernel_ms",
+                                           "cpu_baseline")}
+        out["secondary"] = sec
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -133,30 +133,23 @@ namespace f64m {
 // the fp64 integrator launders once per step, so they are scalar loads next to their uses: as
 // literals all ~44 fp64 coefficients are hoisted out of its step loop into ~88 SGPRs and push the
 // kernel's own scalars into VGPR-lane spills re-read by v_readlane every step.
-constexpr double kCoef[44] = {
-    1.3691488853904128e-12, 2.5678435993488206e-11, 4.4455382718708116e-10, 7.054911620801123e-09,
-    1.01780860092397e-07, 1.321548679014431e-06, 1.5252733804059841e-05, 0.0001540353039338161,
-    0.0013333558146428443, 0.009618129107628477, 0.05550410866482158, 0.24022650695910072, 0.6931471805599453,
-    0.09523809523809523, 0.10526315789473684, 0.11764705882352941, 0.13333333333333333, 0.15384615384615385,
-    0.18181818181818182, 0.2222222222222222, 0.2857142857142857, 0.4, 0.6666666666666666,
-    6.93147180369123816490e-01, 1.90821492927058770002e-10,
-    1.4142135623730951,
-    7.952054001475513e-07, -2.1915353447830217e-05, 0.00046630280576761255, -0.0073704309457143504,
-    0.08214588661112823, -0.5992645293207921, 2.5501640398773455, -5.16771278004997, 3.141592653589793,
-    -1.3878952462213771e-07, 4.303069587032947e-06, -0.0001046381049248457, 0.0019295743094039231,
-    -0.02580689139001406, 0.2353306303588932, -1.3352627688545895, 4.0587121264167685, -4.934802200544679};
-__constant__ double kCoefDev[44] = {
-    1.3691488853904128e-12, 2.5678435993488206e-11, 4.4455382718708116e-10, 7.054911620801123e-09,
-    1.01780860092397e-07, 1.321548679014431e-06, 1.5252733804059841e-05, 0.0001540353039338161,
-    0.0013333558146428443, 0.009618129107628477, 0.05550410866482158, 0.24022650695910072, 0.6931471805599453,
-    0.09523809523809523, 0.10526315789473684, 0.11764705882352941, 0.13333333333333333, 0.15384615384615385,
-    0.18181818181818182, 0.2222222222222222, 0.2857142857142857, 0.4, 0.6666666666666666,
-    6.93147180369123816490e-01, 1.90821492927058770002e-10,
-    1.4142135623730951,
-    7.952054001475513e-07, -2.1915353447830217e-05, 0.00046630280576761255, -0.0073704309457143504,
-    0.08214588661112823, -0.5992645293207921, 2.5501640398773455, -5.16771278004997, 3.141592653589793,
-    -1.3878952462213771e-07, 4.303069587032947e-06, -0.0001046381049248457, 0.0019295743094039231,
-    -0.02580689139001406, 0.2353306303588932, -1.3352627688545895, 4.0587121264167685, -4.934802200544679};
+// One list, two arrays (the literal and the table forms cannot drift apart); kCoefDev has internal
+// linkage, one copy per translation unit that uses it.
+#define WC_F64M_COEFS \
+    1.3691488853904128e-12, 2.5678435993488206e-11, 4.4455382718708116e-10, 7.054911620801123e-09, \
+    1.01780860092397e-07, 1.321548679014431e-06, 1.5252733804059841e-05, 0.0001540353039338161, \
+    0.0013333558146428443, 0.009618129107628477, 0.05550410866482158, 0.24022650695910072, 0.6931471805599453, \
+    0.09523809523809523, 0.10526315789473684, 0.11764705882352941, 0.13333333333333333, 0.15384615384615385, \
+    0.18181818181818182, 0.2222222222222222, 0.2857142857142857, 0.4, 0.6666666666666666, \
+    6.93147180369123816490e-01, 1.90821492927058770002e-10, \
+    1.4142135623730951, \
+    7.952054001475513e-07, -2.1915353447830217e-05, 0.00046630280576761255, -0.0073704309457143504, \
+    0.08214588661112823, -0.5992645293207921, 2.5501640398773455, -5.16771278004997, 3.141592653589793, \
+    -1.3878952462213771e-07, 4.303069587032947e-06, -0.0001046381049248457, 0.0019295743094039231, \
+    -0.02580689139001406, 0.2353306303588932, -1.3352627688545895, 4.0587121264167685, -4.934802200544679
+constexpr double kCoef[44] = {WC_F64M_COEFS};
+static __constant__ double kCoefDev[44] = {WC_F64M_COEFS};
+#undef WC_F64M_COEFS
 enum : int { kExp = 0, kLog = 13, kLn2Hi = 23, kLn2Lo = 24, kSqrt2 = 25, kSin = 26, kCos = 35 };
 struct LitCoef {
     __device__ constexpr double operator[](int i) const { return kCoef[i]; }

@@ -1256,7 +1256,8 @@ int make_args(KArgs& ka, const wc_params* p, int precision, int B, int N, const 
 #ifdef WCSDE_DIAG
 // the fp64 parity path's straight-line elementary functions (wc_device.h, f64m), evaluated alone
 // for tests/test_f64m_gpu.py: 0 exp2(t), 1 rcp(d), 2 log_u24(v), 3 sincospi_v23(v) -> (sin, cos),
-// 4 the fp64 sigmoid Tr<double>::sig(x, mu = 1, s) of (x, s) pairs, 5 sqrt_pos(x)
+// 4 the fp64 sigmoid Tr<double>::sig(x, mu = 1, s) of (x, s) pairs, 5 sqrt_pos(x); 16 + fn for 0, 2, 3:
+// the same function with its coefficients read from the kCoefDev table (TabCoef, WC_F64_TAB = 1)
 __global__ void f64m_kernel(int fn, int64_t n, const void* __restrict__ in, double* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1268,6 +1269,9 @@ __global__ void f64m_kernel(int fn, int64_t n, const void* __restrict__ in, doub
         case 2: out[i] = f64m::log_u24(u[i]); break;
         case 3: f64m::sincospi_v23(u[i], out[2 * i], out[2 * i + 1]); break;
         case 5: out[i] = f64m::sqrt_pos(d[i]); break;
+        case 16: out[i] = f64m::exp2(d[i], f64m::tab_coef()); break;
+        case 18: out[i] = f64m::log_u24(u[i], f64m::tab_coef()); break;
+        case 19: f64m::sincospi_v23(u[i], out[2 * i], out[2 * i + 1], f64m::tab_coef()); break;
         default: out[i] = Tr<double>::sig(d[2 * i], 1.0, d[2 * i + 1]); break;
     }
 }
@@ -1347,7 +1351,7 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N, const doubl
 
 int wc_diag_f64m(int fn, int64_t n, const void* in, double* out, void* stream) {
     wc_clear_err();
-    if (fn < 0 || fn > 5 || n <= 0 || n > (int64_t(1) << 30) || !in || !out)
+    if (!((fn >= 0 && fn <= 5) || fn == 16 || fn == 18 || fn == 19) || n <= 0 || n > (int64_t(1) << 30) || !in || !out)
         return wc_set_err(WC_EINVAL, "wc_diag_f64m: bad arguments");
     hipLaunchKernelGGL(f64m_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream),
                        fn, n, in, out);

@@ -1270,16 +1270,20 @@ int wc_welch_accumulate(int B, int N, const void* E, int e_f64, int64_t ld, int6
                       ld < INT32_MAX / 2 - 8192;
     // fp64 rings: the wave-per-column kernel when sample pairs are 16-B aligned and never split by
     // the ring's wrap (even seg0, slot * nslots and ld; byte offsets within 32 bits)
-    const bool w64 = WC_WELCH_W64 && e_f64 && seg0 % 2 == 0 && (slot * nslots) % 2 == 0 && ld % 2 == 0 &&
-                     ((uintptr_t)E & 15) == 0 && slot * nslots < INT32_MAX / 8 - 8192;
+    bool w64 = WC_WELCH_W64 && e_f64 && seg0 % 2 == 0 && (slot * nslots) % 2 == 0 && ld % 2 == 0 &&
+               ((uintptr_t)E & 15) == 0 && slot * nslots < INT32_MAX / 8 - 8192;
+    // it needs ~160.5 KB of dynamic LDS: if the runtime refuses that, the LDS-Stockham kernel takes the
+    // same inputs (one segment per launch, the same PSD to 3e-16)
+    if (w64 && hipFuncSetAttribute((const void*)welch_wave64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kW64Lds) != hipSuccess) {
+        (void)hipGetLastError();
+        w64 = false;
+    }
     // the LDS-Stockham kernels (fp64 input, unaligned rings) take one segment per launch
     for (int sg = 0; sg < (wave ? 1 : nseg); ++sg) {
         WelchArgs a{B, N, E, ld, slot, nslots, seg0 + (int64_t)sg * (kSeg / 2), wave ? nseg : 1,
                     static_cast<const double*>(workspace), acc};
         if (e_f64 && w64) {
-            hipError_t ea = hipFuncSetAttribute((const void*)welch_wave64_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kW64Lds);
-            if (ea != hipSuccess) return wc_set_err(WC_EHIP, hipGetErrorString(ea));
             hipLaunchKernelGGL(welch_wave64_kernel, dim3(B), dim3(kW64Threads), kW64Lds, st, a);
         } else if (e_f64) {
             constexpr int T = kWelchF64Threads;

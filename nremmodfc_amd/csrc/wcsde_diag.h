@@ -21,7 +21,8 @@ int wc_diag_integrate(int variant, const wc_params* p, int B, int N,
  * device inputs: fn 0 exp2 (double in), 1 rcp (double), 2 log_u24 (uint32 odd
  * v: ln(v 2^-24)), 3 sincospi_v23 (uint32 odd v: out[2i], out[2i+1] = sin, cos
  * of pi v 2^-23), 4 the fp64 sigmoid 1/(1 + e^(-(x - 1) s)) of (x, s) pairs,
- * 5 sqrt_pos (double in, normal positive). */
+ * 5 sqrt_pos (double in, normal positive); 16, 18, 19: fn 0, 2, 3 with the
+ * coefficients read from the constant table (TabCoef, the WC_F64_TAB = 1 form). */
 int wc_diag_f64m(int fn, int64_t n, const void* in, double* out, void* stream);
 
 #ifdef __cplusplus

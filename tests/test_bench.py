@@ -53,8 +53,8 @@ def test_pmc_stamp_is_the_loaded_library():
 
 @pytest.mark.gpu
 def test_bench_json_contract(cuda):
-    out = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--cpu-seconds", "1"],
-                         cwd=ROOT, capture_output=True, text=True, timeout=100)
+    out = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--cpu-seconds", "1",
+                          "--secondary-steps", "2"], cwd=ROOT, capture_output=True, text=True, timeout=180)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
@@ -74,6 +74,13 @@ def test_bench_json_contract(cuda):
     assert "frac" not in r["state_streaming_equiv"]
     assert 0 < r["frac"] < 1.2 and r["issued_mfma"]["dtype"] == "f16"
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["value"] > 0
+    # the 1000-node and reference-precision lines of the same run, each with its own roofline,
+    # kernel times and CPU baseline
+    c5, f64 = d["secondary"]["c5"], d["secondary"]["f64"]
+    assert c5["config"]["nodes"] == 1000 and c5["roofline"]["bound"] == "mfma" and c5["kernel_ms"]["sde"] > 0
+    assert "N=1000" in c5["cpu_baseline"]["sample"] and c5["value"] > 0
+    assert f64["dtype"] == "f64" and f64["config"]["nodes"] == 90 and 0 < f64["roofline"]["frac"] < 1
+    assert f64["cpu_baseline"]["kind"] == "port" and f64["value"] > 0 and f64["kernel_ms"]["welch"] > 0
 
 
 @pytest.mark.gpu
@@ -86,7 +93,9 @@ def test_bench_c5_line_priced_on_mfma(cuda):
     assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and 0 < r["frac"] < 1 and r["peak"] == 2500.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12 and r["operand_stream"]["GBps"] > 0
     o = r["operand_stream"]
-    assert r["binding"] == "operand_stream" and abs(o["frac"] - o["GBps"] / o["peak_GBps"]) < 1e-12
+    assert abs(o["x_ic_gather_peak"] - o["GBps"] / o["ic_gather_peak_GBps"]) < 1e-12
+    if "frac" in o:  # the L2-hit / IC-miss split ceiling, from counters stamped on this library
+        assert 0 < o["l2_hit_rate"] < 1 and abs(o["frac"] - o["GBps"] / o["split_peak_GBps"]) < 1e-12
     assert d["config"]["nodes"] == 1000 and d["config"]["sims_per_gpu"] == 2500
     # the CPU baseline at N = 1000 in the same run (north_star)
     assert d["cpu_baseline"]["value"] > 0 and "N=1000" in d["cpu_baseline"]["sample"]

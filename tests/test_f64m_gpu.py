@@ -121,3 +121,13 @@ def test_f64_sigmoid_error_grows_with_t(diag):
     print(f"TOL f64 sigmoid: max rel {rel.max():.1f} x 2^-53 at |t| <= {t.max():.1f}; "
           f"max (rel - 2.5|t|) {excess.max():.2f} (bound 8); at |t| < 1: {rel[t < 1].max():.2f}")
     assert excess.max() <= 8.0
+
+
+def test_table_coefficients_equal_literals(diag):
+    """WC_F64_TAB = 1 reads the coefficients from the kCoefDev table instead of folding literals in;
+    both come from one list (wc_device.h), so each function gives the same bits either way."""
+    v = np.arange(1, 1 << 24, 2 * 97, dtype=np.uint32)
+    np.testing.assert_array_equal(_run(diag, 18, v, len(v)), _run(diag, 2, v, len(v)))
+    np.testing.assert_array_equal(_run(diag, 19, v, 2 * len(v)), _run(diag, 3, v, 2 * len(v)))
+    t = np.linspace(-1000, 1000, 1 << 18)
+    np.testing.assert_array_equal(_run(diag, 16, t, len(t)), _run(diag, 0, t, len(t)))

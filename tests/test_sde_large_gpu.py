@@ -117,11 +117,13 @@ def _both_paths(sc, G, S, keys, steps, rec_every=20, rec_ld=0, chunks=None):
     return out["default"], out["0"]
 
 
-@pytest.mark.parametrize("N,B", [(1000, 2500), (250, 170), (97, 1)])
+@pytest.mark.parametrize("N,B", [(1000, 2500), (700, 170), (250, 170), (97, 1)])
 def test_persistent_matches_step_kernel(cuda, N, B):
     """Round 2's persistent kernel (state in registers, in-launch E-image hand-off between the
     node-block workgroups of a simulation block) gives the step kernel's bits: same MFMA order,
-    same epilogue arithmetic.  C5 shard, ragged tiles (3 x 2 workgroups), a single simulation."""
+    same epilogue arithmetic.  C5 shard; N = 700 runs the runtime-loop variant (NRP_T = -1) over ten
+    remote chunk pairs, so the 3-stage LDS ring wraps several times; ragged tiles (3 x 2
+    workgroups); a single simulation."""
     sc = _sc(N, 21)
     rng = np.random.default_rng(N)
     G = 0.16 + rng.uniform(-0.1, 0.3, B)
@@ -166,7 +168,7 @@ def test_integrate_status_is_stream_ordered(cuda):
     s = torch.cuda.Stream()
     torch.cuda.synchronize()
     with torch.cuda.stream(s):
-        b.integrate(2000, 2.0, stream=s)  # ~40 ms of persistent work
+        b.integrate(20000, 2.0, stream=s)  # ~0.36 s of persistent work: far longer than the host's return
         ev = torch.cuda.Event()
         ev.record(s)
     assert not ev.query(), "wc_integrate waited for its stream"
