@@ -1071,6 +1071,9 @@ int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int
 
 // X: extra variant bits of every product kernel (V_AII0 when a_ii == 0, the reference's value:
 // -2.2% per C3 launch, bit-identical, tools/diag_variants.py 38 vs 41)
+#ifndef WC_SG2
+#define WC_SG2 1  // CUs < groups <= 2 CUs: two six-wave groups per workgroup (0: one group per workgroup)
+#endif
 template <int X>
 int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) {
     constexpr int V = V_F16X3 | V_KAHAN_A | X;
@@ -1080,12 +1083,22 @@ int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) 
         if (groups <= std::min(kZMaxGroups, cus - kZMinIdle) && ka.nsteps >= 2 * kZK && ka.zbuf &&
             (ka.rec_every == 0 || kZK % ka.rec_every == 0))
             return launch_zmem<X>(ka, sc, ws, st, groups, cus);
-        return launch_v<float, 6, 6, kVarF32 | X>(ka, sc, ws, st);
     }
     // node-major E-only recording (the sweep pipeline's ring): pairs of records per 8-B store
     const bool rec2 = ka.rec_every > 0 && ka.rec_ld > 0 && ka.rec_ld % 2 == 0 && !ka.recI && !ka.recA &&
                       ((uintptr_t)ka.recE & 7) == 0;
     constexpr int V2 = V | V_REC2;
+    if (groups <= 2 * cus) {
+#if WC_SG2
+        // CUs < groups <= 2 CUs (the 4-GPU C3 shard: 313 groups): two groups of six one-tile waves per
+        // workgroup sharing one LDS image, 12 waves per CU.  One group per workgroup put two
+        // six-wave workgroups on groups - CUs of the CUs (1.33 us per step at 5,000 simulations);
+        // this runs 1.15 (tools/time_small.py variant 51, profiles/r06/small_sg2.log)
+        if (groups > cus)
+            return rec2 ? launch_v<float, 6, 6, V2, 1, 2>(ka, sc, ws, st) : launch_v<float, 6, 6, V, 1, 2>(ka, sc, ws, st);
+#endif
+        return launch_v<float, 6, 6, kVarF32 | X>(ka, sc, ws, st);
+    }
     switch (std::min(5, (groups + cus - 1) / cus)) {
 #ifndef WC_NO_MIX
         // three groups per CU: four waves per group with (2, 2, 1, 1) tiles rotated per group (V_MIX)
@@ -1217,6 +1230,15 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 45: return launch_v<float, 6, 6, kVarF32 | V_AII0 | V_NO_MFMA>(ka, sc, ws, st);
         case 46: return launch_v<float, 6, 6, kVarF32 | V_AII0 | V_NO_RNG>(ka, sc, ws, st);
         case 47: return launch_v<float, 6, 6, kVarF32 | V_AII0 | V_NO_MFMA | V_NO_RNG>(ka, sc, ws, st);
+        // 256 < groups <= 512 (the 4-GPU C3 shard): two groups per workgroup sharing the LDS image
+        case 50: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_AII0, 1, 2>(ka, sc, ws, st);
+        case 51: return launch_v<float, 6, 6, V_F16X3 | V_KAHAN_A | V_AII0, 1, 2>(ka, sc, ws, st);
+        case 52: return launch_v<float, 6, 4, V_F16X3 | V_KAHAN_A | V_AII0 | V_MIX, 1, 2>(ka, sc, ws, st);
+        case 53: return launch_v<float, 6, 2, V_F16X3 | V_KAHAN_A | V_AII0, 1, 2>(ka, sc, ws, st);
+        // 2 CUs < groups <= 3 CUs (the 2-GPU shard: 625 groups): three groups per workgroup
+        case 54: return launch_v<float, 6, 6, V_F16X3 | V_KAHAN_A | V_AII0, 1, 3>(ka, sc, ws, st);
+        case 55: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_AII0, 1, 3>(ka, sc, ws, st);
+        case 56: return launch_v<float, 6, 4, V_F16X3 | V_KAHAN_A | V_AII0 | V_MIX, 1, 3>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }

@@ -40,6 +40,12 @@ def test_full_batch_permutation_and_shard_invariance(cuda, sc90):
     sb.integrate(300, 0.05)
     sb.integrate(300, 2.0)
     assert np.array_equal(_state(sb), ref[:, shard])
+    # rank 1 of 4: 5,000 simulations, the two-groups-per-workgroup kernel
+    shard = np.arange(B)[np.arange(B) % 4 == 1]
+    sb = Batch(sc90, G[shard], S[shard], keys[shard], p, precision="f32")
+    sb.integrate(300, 0.05)
+    sb.integrate(300, 2.0)
+    assert np.array_equal(_state(sb), ref[:, shard])
 
 
 def test_full_batch_launch_chunking(cuda, sc90):

@@ -164,7 +164,7 @@ def test_f32_tracks_f64_statistics(cuda, sc90):
     assert np.abs(out["f32"] - out["f64"]).max() < 5e-3  # observed 6.6e-4
 
 
-@pytest.mark.parametrize("B", [9000, 20000])
+@pytest.mark.parametrize("B", [5000, 9000, 20000])
 def test_grouped_kernel_matches_register_kernel(cuda, sc90, B):
     """Large batches run the one-workgroup-per-CU kernel (SG groups of 16 sims
     sharing the LDS connectome image); its trajectories equal the register-
@@ -192,12 +192,11 @@ def test_grouped_kernel_matches_register_kernel(cuda, sc90, B):
     assert d.max() <= 3e-5 and np.sqrt(np.mean(d ** 2)) <= 3e-6  # observed max 3.4e-6, rms 2.9e-7 (400 steps)
 
 
-@pytest.mark.parametrize("nsteps", [400, 380, 20])
-def test_grouped_kernel_ring_records(cuda, sc90, nsteps):
+@pytest.mark.parametrize("B,nsteps", [(9000, 400), (9000, 380), (9000, 20), (5000, 380)])
+def test_grouped_kernel_ring_records(cuda, sc90, B, nsteps):
     """The pipeline's node-major ring (rec_ld > 0) through the grouped kernel with
     paired-record stores, including an odd record count (buffer flushed at exit):
-    equal to the time-major records of the same trajectory."""
-    B = 9000
+    equal to the time-major records of the same trajectory (B = 5000: the two-group workgroups)."""
     rng = np.random.default_rng(7)
     G = 0.16 + rng.uniform(-0.1, 0.3, B)
     S = 7.68 + rng.uniform(-0.2, 0.2, B)

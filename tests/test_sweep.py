@@ -59,6 +59,29 @@ def test_shard_is_reference_round_robin():
     assert all(s.index % 7 == r for r, p in enumerate(parts) for s in p)
 
 
+def test_c4_job_round_robin_over_both_tables():
+    """BASELINE config 4 as one job: `maps --map-ids 1 1 2 2 --seeds 50 --seed0 0` lists the real-map
+    and the shuffled sweeps (2 x 20,000, whole_sweep_both_maps.py:27-28,92-108) and deals their
+    concatenation round robin, so each of 8 ranks holds 5,000 simulations, half of each table;
+    one table alone is the reference's `sim % threads == rank`."""
+    args = sweep.argparse.Namespace(kind="maps", map_ids=[1, 1, 2, 2], seeds=50, seed0=0, grid="shipped", nodes=90,
+                                    tag=None, limit=None)
+    jobs = sweep._jobs(args)
+    assert [len(j[0]) for j in jobs] == [20000, 20000]
+    assert [t for _, t in jobs] == ["sweep_deltamaps_from_homoW_fromG0.16_sigma7.68_maps_1_1",
+                                    "sweep_deltaSHUFFLED_from_homoW_fromG0.16_sigma7.68_maps_2_2"]
+    for world in (1, 2, 4, 8, 3):
+        shards = [sweep.job_shards(jobs, r, world) for r in range(world)]
+        sizes = [sum(len(p) for p in sh) for sh in shards]
+        assert max(sizes) - min(sizes) <= 1 and sum(sizes) == 40000
+        for k in (0, 1):
+            assert sorted(s.index for sh in shards for s in sh[k]) == list(range(20000))
+        if world == 8:
+            assert sizes == [5000] * 8 and all(len(sh[0]) == len(sh[1]) == 2500 for sh in shards)
+    one = sweep._jobs(sweep.argparse.Namespace(**dict(vars(args), map_ids=[2, 2])))
+    assert [s.index for s in sweep.job_shards(one, 3, 7)[0]] == [s.index for s in sweep.shard(one[0][0], 3, 7)]
+
+
 def _shipped(kind):
     import pandas as pd
     return pd.read_csv(os.path.join(GOLD, f"shipped_{kind}_head.csv"))
@@ -203,6 +226,22 @@ def test_sweep_main_short(tmp_path, cuda):
     with open(os.path.join(out, "temp", "t_rank0_perf.jsonl")) as f:  # one perf line per invocation
         perf = [json.loads(line) for line in f]
     assert [p["sims"] for p in perf] == [6, 0] and perf[0]["node_steps_per_s"] > 0
+
+
+@pytest.mark.gpu
+def test_c4_one_job_equals_the_two_sweeps(tmp_path, cuda):
+    """The C4 job (both map-id pairs in one run, one batch holding simulations of both tables) writes
+    the same two tables, byte for byte, as the two sweeps run one after the other."""
+    a, b = str(tmp_path / "job"), str(tmp_path / "sep")
+    sweep.main(["maps", "--map-ids", "1", "1", "2", "2", "--seeds", "1", "--seed0", "0", "--short", "--limit", "10",
+                "--out", a])
+    for ids in (["1", "1"], ["2", "2"]):
+        sweep.main(["maps", "--map-ids", *ids, "--seeds", "1", "--seed0", "0", "--short", "--limit", "10", "--out", b])
+    for t in ("sweep_deltamaps_from_homoW_fromG0.16_sigma7.68_maps_1_1",
+              "sweep_deltaSHUFFLED_from_homoW_fromG0.16_sigma7.68_maps_2_2"):
+        with open(os.path.join(a, t + ".txt"), "rb") as f, open(os.path.join(b, t + ".txt"), "rb") as g:
+            x, y = f.read(), g.read()
+        assert x == y and x.count(b"\n") == 11
 
 
 @pytest.mark.gpu
