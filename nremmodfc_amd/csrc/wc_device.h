@@ -372,6 +372,34 @@ __device__ __forceinline__ void split2h_pair(const float v[2], uint32_t& hi, uin
     lo = lb;
 }
 
+// fp16 three-part split of v * 2^10 (the V_F16X6 A/B): hi = fp16(x), r = x - hi exact in fp32 (one
+// v_fma_mix_f32 per value), mid = fp16(r), lo = fp16(r - mid) (v_fma_mix{lo,hi}_f16, rounded once)
+template <bool PRE = false>
+__device__ __forceinline__ void split3h(const float v[4], f16x4& hi, f16x4& mid, f16x4& lo) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const f2 x = PRE ? (f2){v[2 * p], v[2 * p + 1]} : (f2){v[2 * p], v[2 * p + 1]} * 1024.0f;
+        const h2 h = __builtin_convertvector(x, h2);
+        float r0, r1;
+        asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r0) : "v"(x[0]), "v"(h));
+        asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r1) : "v"(x[1]), "v"(h));
+        const f2 r = {r0, r1};
+        const h2 m = __builtin_convertvector(r, h2);
+        uint32_t lb;
+        asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(lb) : "v"(r[0]), "v"(m));
+        asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(lb) : "v"(r[1]), "v"(m));
+        const h2 l = __builtin_bit_cast(h2, lb);
+        hi[2 * p] = h[0];
+        hi[2 * p + 1] = h[1];
+        mid[2 * p] = m[0];
+        mid[2 * p + 1] = m[1];
+        lo[2 * p] = l[0];
+        lo[2 * p + 1] = l[1];
+    }
+}
+
 // Plasticity variable a_ie: fp64, or a compensated fp32 pair (increments of
 // ~1e-6 on a ~2.5 are below fp32 half-ulp: plain fp32 would drop them).
 template <bool kPair> struct AccA;

@@ -128,11 +128,12 @@ __global__ void build_frag_bf16(const double* __restrict__ sc, int N, bf16x8* __
 
 // the two scale floats follow the fp16 image (inside the fp32 workspace, which is
 // sized for the 3-part bf16 image)
-__host__ __device__ constexpr size_t hf_scale_offset(int NT) { return (size_t)NT * (NT / 2) * 2 * 64 * 16 / 4; }
+// (P = 3: the three-part image of V_F16X6; frag_bytes leaves room for the scales behind it)
+__host__ __device__ constexpr size_t hf_scale_offset(int NT, int P = 2) { return (size_t)NT * (NT / 2) * P * 64 * 16 / 4; }
 
 // fp16 x3: frag[((T*NC + c)*2 + p)*64 + lane][jj] = part p of CM[..] sA, hi = fp16(x),
 // lo = fp16(x - hi) (same element order as build_frag_bf16)
-template <int NT>
+template <int NT, int P = 2>
 __global__ void build_frag_f16(const double* __restrict__ sc, int N, const float* __restrict__ scl,
                                f16x8* __restrict__ frag) {
     constexpr int NC = NT / 2;
@@ -142,17 +143,19 @@ __global__ void build_frag_f16(const double* __restrict__ sc, int N, const float
     const int T = tc / NC, c = tc % NC;
     const double sA = scl[0];
     const int row = 16 * T + (lane & 15);
-    f16x8 part[2];
+    f16x8 part[P];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
         const int col = 16 * (2 * c + (jj >> 2)) + 4 * (lane >> 4) + (jj & 3);
         const double x = (row < N && col < N) ? sc[(size_t)row * N + col] * sA : 0.0;
         const _Float16 h = (_Float16)(float)x;
+        const double r = x - (double)(float)h;
         part[0][jj] = h;
-        part[1][jj] = (_Float16)(float)(x - (double)(float)h);
+        part[1][jj] = (_Float16)(float)r;
+        if constexpr (P == 3) part[2][jj] = (_Float16)(float)(r - (double)(float)part[1][jj]);
     }
 #pragma unroll
-    for (int p = 0; p < 2; ++p) frag[(size_t)(tc * 2 + p) * 64 + lane] = part[p];
+    for (int p = 0; p < P; ++p) frag[(size_t)(tc * P + p) * 64 + lane] = part[p];
 }
 
 // ---------------- packed fp32 cell pair (the fp32 product update) ----------------
@@ -250,6 +253,11 @@ enum : int {
     V_ZMEM = 131072,  // the raw normals come precomputed from zbuf (zblock_kernel on otherwise idle CUs)
     V_HALF2 = 262144, // NW = 2 NT: two waves per node tile, each updating two of a lane's four rows
                       // (both run the tile's coupling MFMAs; with V_ZMEM, so no Philox is repeated)
+    V_F16X6 = 1048576, // A/B: three-part fp16 operands (E and CM each hi + mid + lo), six cross terms
+                       // down to 2^-22 (>= 24 significant bits of both operands)
+    V_ZPAIR = 524288, // SG = 2, V_ZMEM, one workgroup per CU: workgroups < zgen_b0 integrate two groups,
+                      // the others one group while their second group's waves draw the next block's
+                      // normals, one step's share per step between the workgroup's barriers
 };
 
 constexpr bool kFragRegs_(int var) { return (var & V_FRAG_REGS) != 0; }
@@ -265,13 +273,14 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     static_assert(kMix ? (NT == 6 && NW == 4) : kHalf ? (NW == 2 * NT && SG == 1) : NT % NW == 0, "NW must divide NT");
     constexpr int OT = kMix ? 2 : kHalf ? 1 : NT / NW;  // tile slots per wave
     constexpr int RW = kHalf ? 2 : 4;                    // rows of a lane's 4 (one MFMA column quad) owned
-    constexpr bool kHf = (VAR & V_F16X3) != 0;
-    constexpr int kTerms = (VAR & V_BF16X6) ? 6 : (VAR & V_BF16X3) ? 3 : kHf ? 3 : 0;
+    constexpr bool kHf3 = (VAR & V_F16X6) != 0;
+    constexpr bool kHf = (VAR & (V_F16X3 | V_F16X6)) != 0;
+    constexpr int kTerms = (VAR & V_BF16X6) ? 6 : (VAR & V_BF16X3) ? 3 : kHf3 ? 6 : kHf ? 3 : 0;
     constexpr bool kBf = kTerms > 0;  // 16-bit split coupling (bf16 or fp16 parts)
     static_assert(!kBf || (sizeof(Real) == 4 && NT % 2 == 0), "split coupling: fp32, even tile count");
     constexpr int NC = NT / 2;  // 16-bit k-chunks (2 tiles = 32 nodes)
     constexpr int NP = kTerms == 6 ? 3 : 2;
-    constexpr int PS = kHf ? 2 : 3;  // parts per chunk in the images
+    constexpr int PS = (kHf && !kHf3) ? 2 : 3;  // parts per chunk in the images
     constexpr bool kFragRegs = (VAR & V_FRAG_REGS) != 0;
     constexpr bool kRng = (VAR & V_NO_RNG) == 0;
     constexpr bool kMfma = (VAR & V_NO_MFMA) == 0;
@@ -288,14 +297,16 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     constexpr bool kLean = kFast && kPk && (VAR & V_LEAN) != 0;
     constexpr bool kAii0 = kFast && kPk && (VAR & V_AII0) != 0;
     constexpr bool kZMem = kFast && kPk && kRng && (VAR & V_ZMEM) != 0;
-    static_assert(!kHalf || (kZMem && kHf), "V_HALF2: the fp16x3 packed path with precomputed normals");
+    static_assert(!kHalf || (kZMem && kHf && !kHf3), "V_HALF2: the fp16x3 packed path with precomputed normals");
+    constexpr bool kZPair = (VAR & V_ZPAIR) != 0;
+    static_assert(!kZPair || (kZMem && SG == 2 && NW > 1 && !kHalf), "V_ZPAIR: two groups, normals from zbuf");
     constexpr float kEsc = kEs ? 1024.0f : 1.0f, kEinv = kEs ? 0x1p-10f : 1.0f;
     // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
     constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
     constexpr int kFragUnits = kBf ? NT * NC * PS : NT * NT;  // 16-B (bf16x8 / real4 f32) or 32-B units
 
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if constexpr ((VAR & V_ZMEM) != 0) {
+    if constexpr ((VAR & V_ZMEM) != 0 && !kZPair) {
         if ((int)blockIdx.x >= a.zgen_b0) {  // generator workgroup: the next block's normals, grid-stride
             const uint32_t total = (uint32_t)a.zgen_K * NT * (uint32_t)a.zBp * 4u;
             const uint32_t stride = (gridDim.x - a.zgen_b0) * blockDim.x;
@@ -319,7 +330,12 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     const int lane = threadIdx.x & 63;
     const int w = SG == 1 ? threadIdx.x >> 6 : (threadIdx.x >> 6) % NW;
     const int j = lane & 15, g = lane >> 4;
-    const int b = a.b0 + (blockIdx.x * SG + grp) * kSims + j;
+    // V_ZPAIR: workgroup i < zgen_b0 holds groups 2i, 2i + 1; a later one group zgen_b0 + i and,
+    // in its second group's waves, a normals generator (no simulation: b past the batch)
+    const bool zgen = kZPair && (int)blockIdx.x >= a.zgen_b0 && grp == 1;
+    const int gidx = !kZPair ? (int)blockIdx.x * SG + grp
+                   : (int)blockIdx.x < a.zgen_b0 ? 2 * (int)blockIdx.x + grp : a.zgen_b0 + (int)blockIdx.x;
+    const int b = zgen ? a.B + j : a.b0 + gidx * kSims + j;
     const bool live = b < a.B;
     const int bb = live ? b : a.B - 1;  // tail lanes mirror the last sim, never store
     const int N = a.N;
@@ -369,7 +385,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     const uint64_t key = a.keys[bb];
     // fp16 coupling: the MFMA sums CM sA x E 2^10; 1 / (2^10 sA) is folded into G (exact)
     Real gscale = 1;
-    if constexpr (kHf) gscale = reinterpret_cast<const float*>(a.frag)[hf_scale_offset(NT) + 1];
+    if constexpr (kHf) gscale = reinterpret_cast<const float*>(a.frag)[hf_scale_offset(NT, PS) + 1];
 
     // ---- own state and per-node parameters ----
     constexpr int PT = kParamRegs ? OT : 1;
@@ -403,7 +419,12 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     bf16x4 h0, m0, l0, h1, m1, l1;
-                    if constexpr (kHf) {
+                    if constexpr (kHf3) {
+                        split3h<kEs>(E[2 * c], reinterpret_cast<f16x4&>(h0), reinterpret_cast<f16x4&>(m0),
+                                     reinterpret_cast<f16x4&>(l0));
+                        split3h<kEs>(E[2 * c + 1], reinterpret_cast<f16x4&>(h1), reinterpret_cast<f16x4&>(m1),
+                                     reinterpret_cast<f16x4&>(l1));
+                    } else if constexpr (kHf) {
                         split2h<kEs>(E[2 * c], reinterpret_cast<f16x4&>(h0), reinterpret_cast<f16x4&>(m0));
                         split2h<kEs>(E[2 * c + 1], reinterpret_cast<f16x4&>(h1), reinterpret_cast<f16x4&>(m1));
                     } else {
@@ -436,7 +457,10 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                     if (!owned(u)) continue;
                     const int t = TL(u);  // chunk t/2, half t&1 (runtime: address arithmetic only)
                     bf16x4 hmo[3];
-                    if constexpr (kHf) split2h<kEs>(E[u], reinterpret_cast<f16x4&>(hmo[0]), reinterpret_cast<f16x4&>(hmo[1]));
+                    if constexpr (kHf3)
+                        split3h<kEs>(E[u], reinterpret_cast<f16x4&>(hmo[0]), reinterpret_cast<f16x4&>(hmo[1]),
+                                     reinterpret_cast<f16x4&>(hmo[2]));
+                    else if constexpr (kHf) split2h<kEs>(E[u], reinterpret_cast<f16x4&>(hmo[0]), reinterpret_cast<f16x4&>(hmo[1]));
                     else split3(E[u], hmo[0], hmo[1], hmo[2]);
 #pragma unroll
                     for (int p = 0; p < NP; ++p) x4[(((t >> 1) * PS + p) * 64 + lane) * 2 + (t & 1)] = hmo[p];
@@ -450,6 +474,45 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         }
     };
     if constexpr (!kFragRegs) __syncthreads();  // A-operand image staged
+    if constexpr (kZPair) {
+        if (zgen) {
+            // the integrating group's barriers, one for publish(0) and one per step, are matched one
+            // for one (raw s_barrier: nothing of this wave's needs ordering against them, and its
+            // normals stores must not be waited for at every step); between two of them this wave
+            // draws its share of one step of the next block: the same quads every step (key and
+            // quad index loaded once), quad_normals_pk and the zbuf layout of zblock_kernel
+            constexpr int kGI = 3;  // quads per thread and step at most (host: zpair_shape)
+            const uint32_t per_step = (uint32_t)NT * (uint32_t)a.zBp * 4u;
+            const uint32_t nthr = (gridDim.x - (uint32_t)a.zgen_b0) * (NW * 64u);
+            const uint32_t me = (blockIdx.x - (uint32_t)a.zgen_b0) * (NW * 64u) + (threadIdx.x - NW * 64u);
+            uint64_t gkey[kGI];
+            uint32_t gquad[kGI];
+#pragma unroll
+            for (int k = 0; k < kGI; ++k) {
+                const uint32_t i = me + (uint32_t)k * nthr;
+                const uint32_t bq = (i >> 2) % (uint32_t)a.zBp, tq = (i >> 2) / (uint32_t)a.zBp;
+                gquad[k] = 4u * tq + (i & 3u);
+                gkey[k] = i < per_step ? a.keys[bq < (uint32_t)a.B ? bq : a.B - 1] : 0;
+            }
+            __builtin_amdgcn_s_barrier();
+            float4* zo = a.zbuf_next + me;
+            for (int s = 0; s < a.nsteps; ++s) {
+                if (s < a.zgen_K) {
+#pragma unroll
+                    for (int k = 0; k < kGI; ++k) {
+                        if (me + (uint32_t)k * nthr < per_step) {
+                            f2v zp[2];
+                            quad_normals_pk((uint64_t)(a.zgen_step0 + s), gquad[k], gkey[k], zp);
+                            zo[(size_t)k * nthr] = make_float4(zp[0].x, zp[0].y, zp[1].x, zp[1].y);
+                        }
+                    }
+                    zo += per_step;
+                }
+                __builtin_amdgcn_s_barrier();
+            }
+            return;
+        }
+    }
     publish(0);
 
     Real a_ee = (Real)a.a_ee, a_ei = (Real)a.a_ei, a_ii = (Real)a.a_ii;
@@ -637,8 +700,13 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                         if constexpr (kFragRegs) f[p] = F16[u][c][p];
                         else f[p] = l16[((TL(u) * NC + c) * PS + p) * 64 + fl];
                     }
-                    if constexpr (kHf) {  // small terms first: 2^-11 (lo.hi, hi.lo), 1 (hi.hi)
+                    if constexpr (kHf) {  // small terms first: [2^-22 (lo.hi, mid.mid, hi.lo)], 2^-11 (lo.hi, hi.lo), 1 (hi.hi)
                         typedef f16x8 h8;
+                        if constexpr (kHf3) {
+                            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[2], (h8)xe[0], acc[u], 0, 0, 0);
+                            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[1], (h8)xe[1], acc[u], 0, 0, 0);
+                            acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[0], (h8)xe[2], acc[u], 0, 0, 0);
+                        }
                         acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[1], (h8)xe[0], acc[u], 0, 0, 0);
                         acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[0], (h8)xe[1], acc[u], 0, 0, 0);
                         acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_f16((h8)f[0], (h8)xe[0], acc[u], 0, 0, 0);
@@ -920,20 +988,21 @@ int tiles_for(int N) { return (N + 15) / 16; }
 template <typename Real, int NT, int NW, int VAR, int MINW = 1, int SG = 1>
 int launch_v(const KArgs& ka, const double* sc, void* ws, hipStream_t st, bool prep = true, int extra_blocks = 0,
              size_t lds_floor = 0, int g0 = 0, int ng = -1) {
-    constexpr bool hf = (VAR & V_F16X3) != 0;
+    constexpr bool hf = (VAR & (V_F16X3 | V_F16X6)) != 0;
+    constexpr int HP = (VAR & V_F16X6) ? 3 : 2;  // fp16 parts per operand
     constexpr bool bf = (VAR & (V_BF16X6 | V_BF16X3)) != 0;
     constexpr bool frag_regs = (VAR & V_FRAG_REGS) != 0;
     size_t lds;
     if constexpr (hf) {
         const int total = NT * (NT / 2) * 64;
-        float* scl = static_cast<float*>(ws) + hf_scale_offset(NT);
+        float* scl = static_cast<float*>(ws) + hf_scale_offset(NT, HP);
         if (prep) {  // (prep = false: a later launch of the same call reuses the image)
             hipLaunchKernelGGL(coupling_scale_kernel, dim3(1), dim3(1024), 0, st, sc, ka.N, scl);
-            hipLaunchKernelGGL((build_frag_f16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
+            hipLaunchKernelGGL((build_frag_f16<NT, HP>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
                                static_cast<const float*>(scl), static_cast<f16x8*>(ws));
         }
-        lds = (frag_regs ? 0 : (size_t)NT * (NT / 2) * 2 * 64 * 16) +
-              (NW > 1 ? (size_t)SG * 2 * (NT / 2) * 2 * 64 * 16 : 0);
+        lds = (frag_regs ? 0 : (size_t)NT * (NT / 2) * HP * 64 * 16) +
+              (NW > 1 ? (size_t)SG * 2 * (NT / 2) * HP * 64 * 16 : 0);
     } else if constexpr (bf) {
         const int total = NT * (NT / 2) * 64;
         hipLaunchKernelGGL((build_frag_bf16<NT>), dim3((total + 255) / 256), dim3(256), 0, st, sc, ka.N,
@@ -978,7 +1047,7 @@ size_t frag_bytes(int N, int precision) {
         return (size_t)nt * nt * 64 * 4 * 8;
     }
     const int nt = (tiles_for(N) + 1) & ~1;  // bf16 k-chunks pair tiles
-    return (size_t)nt * (nt / 2) * 3 * 64 * 16;
+    return (size_t)nt * (nt / 2) * 3 * 64 * 16 + 256;  // (+ the fp16 scales behind a three-part image)
 }
 
 // the two normals blocks of the small-batch path follow the fp32 connectome image (256-B aligned)
@@ -1006,11 +1075,24 @@ size_t zmem_block_bytes(int B) {
 }
 
 // B and N for which the small-batch path precomputes its normals (fp32, 81 <= N <= 96)
+// V_ZPAIR regime: CUs < groups <= kZPairMax x CUs (the generators, one per one-group workgroup,
+// draw at most ~2.5 quads per thread and step)
+// (1.25: <= 1.67 quads per generator thread and step.  Measured: 4,100 simulations 0.973 us per step
+// against 1.138 for the plain two-group kernel, 5,000 1.051 vs 1.144, but 5,700 (357 groups, 2.3
+// quads per thread) 1.181 vs 1.144: the generators set the step; profiles/r06/zpair.log)
+constexpr double kZPairMax = 1.25;
+bool zpair_shape(int groups, int cus) {
+    const char* env = getenv("WCSDE_ZPAIR");
+    if (env && env[0] == '0') return false;
+    return groups > cus && groups <= (int)(kZPairMax * cus);
+}
+
 bool zmem_eligible_shape(int B, int N) {
     const char* env = getenv("WCSDE_ZMEM");
     if (env && env[0] == '0') return false;
     const int groups = (B + kSims - 1) / kSims;
-    return tiles_for(N) == kMaxTiles && groups <= std::min(kZMaxGroups, cu_count() - kZMinIdle);
+    const int cus = cu_count();
+    return tiles_for(N) == kMaxTiles && (groups <= std::min(kZMaxGroups, cus - kZMinIdle) || zpair_shape(groups, cus));
 }
 
 int cu_count() {
@@ -1029,7 +1111,7 @@ int cu_count() {
 // Many groups: ONE workgroup per CU holding SG = ceil(groups / CUs) groups that
 // share the LDS connectome image (<= 155 / 128 registers): every simulation is
 // resident at once (a single round of workgroups, no tail) at 3-4 waves/SIMD.
-template <int X>
+template <int X, bool PAIR = false>
 int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int groups, int cus) {
     // one launch per block of kZK steps on the caller's stream, ONE workgroup per CU (an LDS floor
     // above half the CU's LDS): the first `groups` workgroups integrate this block from the buffered
@@ -1049,7 +1131,7 @@ int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int
         kb.zbuf = zb[k & 1];
         kb.zBp = Bp;
         kb.zbuf_next = zb[(k + 1) & 1];
-        kb.zgen_b0 = groups;
+        kb.zgen_b0 = PAIR ? groups - cus : groups;  // PAIR: the two-group workgroups come first
         kb.zgen_step0 = kb.step0 + kZK;
         kb.zgen_K = k + 1 < nb ? std::min(kZK, ka.nsteps - (k + 1) * kZK) : 0;
         if (R) {  // this block's first record row (kZK is a multiple of rec_every)
@@ -1059,11 +1141,22 @@ int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int
             if (ka.recI) kb.recI = static_cast<float*>(ka.recI) + off;
             if (ka.recA) kb.recA = static_cast<float*>(ka.recA) + off;
         }
+        int rc;
+        if constexpr (PAIR) {
+            // one workgroup per CU: groups - cus of them with two groups, the rest one group + generator
+            constexpr int V = V_F16X3 | V_KAHAN_A | X | V_ZMEM | V_ZPAIR;
+            const bool rec2 = ka.rec_every > 0 && ka.rec_ld > 0 && ka.rec_ld % 2 == 0 && !ka.recI && !ka.recA &&
+                              ((uintptr_t)ka.recE & 7) == 0;
+            const int extra = cus - (groups + 1) / 2;
+            rc = rec2 ? launch_v<float, 6, 6, V | V_REC2, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024)
+                      : launch_v<float, 6, 6, V, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024);
+        } else {
 #if WC_ZMEM_HALF
-        const int rc = launch_v<float, 6, 12, kVarF32 | X | V_ZMEM | V_HALF2>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);
+        rc = launch_v<float, 6, 12, kVarF32 | X | V_ZMEM | V_HALF2>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);
 #else
-        const int rc = launch_v<float, 6, 6, kVarF32 | X | V_ZMEM>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);
+        rc = launch_v<float, 6, 6, kVarF32 | X | V_ZMEM>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);
 #endif
+        }
         if (rc != WC_OK) return rc;
     }
     return wc_hip_check("wc_integrate (normals-block path)");
@@ -1089,6 +1182,8 @@ int launch_f32_nt6(const KArgs& ka, const double* sc, void* ws, hipStream_t st) 
                       ((uintptr_t)ka.recE & 7) == 0;
     constexpr int V2 = V | V_REC2;
     if (groups <= 2 * cus) {
+        if (zpair_shape(groups, cus) && ka.nsteps >= 2 * kZK && ka.zbuf && (ka.rec_every == 0 || kZK % ka.rec_every == 0))
+            return launch_zmem<X, true>(ka, sc, ws, st, groups, cus);
 #if WC_SG2
         // CUs < groups <= 2 CUs (the 4-GPU C3 shard: 313 groups): two groups of six one-tile waves per
         // workgroup sharing one LDS image, 12 waves per CU.  One group per workgroup put two
@@ -1239,6 +1334,8 @@ int launch_diag(int variant, const KArgs& ka, const double* sc, void* ws, hipStr
         case 54: return launch_v<float, 6, 6, V_F16X3 | V_KAHAN_A | V_AII0, 1, 3>(ka, sc, ws, st);
         case 55: return launch_v<float, 6, 3, V_F16X3 | V_KAHAN_A | V_AII0, 1, 3>(ka, sc, ws, st);
         case 56: return launch_v<float, 6, 4, V_F16X3 | V_KAHAN_A | V_AII0 | V_MIX, 1, 3>(ka, sc, ws, st);
+        // the C3 product configuration (= 41, time-major records as the bench) with the >= 24-bit coupling
+        case 58: return launch_v<float, 6, 3, V_F16X6 | V_KAHAN_A | V_AII0, 1, 5>(ka, sc, ws, st);
         default: return wc_set_err(WC_EINVAL, "unknown diagnostic variant");
     }
 }
