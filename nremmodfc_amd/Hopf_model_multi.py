@@ -8,8 +8,9 @@ Callers mutate the globals and call Sim(), as optimize_SC_Hopf.py:18-39 does.
 The Euler-Maruyama loop (Hopf_model :46-59, Noise :63-69, Sim :79-156) runs in
 libwcsde.so (wc_hopf_integrate, csrc/wc_hopf.hip), fp64, batched:
 sim_batch(seeds) integrates one simulation per seed in one launch, which is what
-the optimiser (nremmodfc_amd.optimize_sc) uses.  Hopf_model and Noise are fused
-into that kernel and raise if called on their own.
+the optimiser (nremmodfc_amd.optimize_sc) uses.  Hopf_model and Noise, fused into
+that kernel, are also callable on their own (one drift / one noise evaluation, as
+device tensor operations; the noise from torch's device generator seeded by set_seed).
 
 Deliberate deviations:
   * noise: the build's Philox stream keyed by the seed (numba's per-thread RNG
@@ -68,18 +69,44 @@ G = 0.25
 seed = 0
 
 
-def Hopf_model(x, y, t):
-    raise NotImplementedError("Hopf_model is fused into wc_hopf_integrate (libwcsde.so); call Sim()")
+def _col(v, device):
+    return torch.as_tensor(np.asarray(v, dtype=np.float64).reshape(nnodes, 1), device=device)
 
 
-def Noise(x, y, t):
-    raise NotImplementedError("Noise is drawn inside wc_hopf_integrate (Philox stream); call Sim()")
+def Hopf_model(x, y, t, device="cuda"):
+    """Hopf_model_multi.py:46-59: the drift of one Euler step at the column states x, y (nnodes, 1)
+    -> hstack((x_dot, y_dot)) (nnodes, 2).  IsynX_i = G / norm sum_j M_ij (x_j - x_i) (:50-54), the
+    same sums wc_hopf_integrate forms per step."""
+    X, Y = _col(x, device), _col(y, device)
+    gm = torch.as_tensor(_check_m(), device=device) * (G / norm)
+    isx = gm @ X - gm.sum(1, keepdim=True) * X
+    isy = gm @ Y - gm.sum(1, keepdim=True) * Y
+    r2 = X * X + Y * Y
+    xd = (a - r2) * X - w * Y + isx
+    yd = (a - r2) * Y + w * X + isy
+    return torch.cat((xd, yd), dim=1).cpu().numpy()
+
+
+_noise_gen = {}
+
+
+def Noise(x, y, t, device="cuda"):
+    """Hopf_model_multi.py:63-69: beta * N(0, 1) for x and y of every node -> (nnodes, 2), drawn
+    from torch's generator on the device, seeded by set_seed (Sim() itself uses the kernel's
+    Philox stream keyed by the seed)."""
+    gen = _noise_gen.get(str(device))
+    if gen is None:
+        gen = _noise_gen[str(device)] = torch.Generator(device=device)
+        gen.manual_seed(int(seed))
+    z = torch.randn((nnodes, 2), generator=gen, dtype=torch.float64, device=device)
+    return (z * beta).cpu().numpy()
 
 
 def set_seed(s):
-    """Hopf_model_multi.py:73-76: the seed of the next Sim()."""
+    """Hopf_model_multi.py:73-76: the seed of the next Sim() (and of Noise's generator)."""
     global seed
     seed = s
+    _noise_gen.clear()
     return s
 
 

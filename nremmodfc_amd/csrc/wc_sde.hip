@@ -255,6 +255,8 @@ enum : int {
                       // (both run the tile's coupling MFMAs; with V_ZMEM, so no Philox is repeated)
     V_F16X6 = 1048576, // A/B: three-part fp16 operands (E and CM each hi + mid + lo), six cross terms
                        // down to 2^-22 (>= 24 significant bits of both operands)
+    V_ZSELF = 2097152, // with V_ZPAIR: the one-group workgroups draw their own normals in-kernel; the
+                       // generators draw only the two-group workgroups' (the first 2 zgen_b0 groups)
     V_ZPAIR = 524288, // SG = 2, V_ZMEM, one workgroup per CU: workgroups < zgen_b0 integrate two groups,
                       // the others one group while their second group's waves draw the next block's
                       // normals, one step's share per step between the workgroup's barriers
@@ -300,6 +302,7 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     static_assert(!kHalf || (kZMem && kHf && !kHf3), "V_HALF2: the fp16x3 packed path with precomputed normals");
     constexpr bool kZPair = (VAR & V_ZPAIR) != 0;
     static_assert(!kZPair || (kZMem && SG == 2 && NW > 1 && !kHalf), "V_ZPAIR: two groups, normals from zbuf");
+    constexpr bool kZSelf = kZPair && (VAR & V_ZSELF) != 0;
     constexpr float kEsc = kEs ? 1024.0f : 1.0f, kEinv = kEs ? 0x1p-10f : 1.0f;
     // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
     constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
@@ -482,20 +485,23 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             // draws its share of one step of the next block: the same quads every step (key and
             // quad index loaded once), quad_normals_pk and the zbuf layout of zblock_kernel
             constexpr int kGI = 3;  // quads per thread and step at most (host: zpair_shape)
-            const uint32_t per_step = (uint32_t)NT * (uint32_t)a.zBp * 4u;
+            // (V_ZSELF: only the simulations of the two-group workgroups, the first Bq of the batch)
+            const uint32_t Bq = kZSelf ? 2u * (uint32_t)a.zgen_b0 * kSims : (uint32_t)a.zBp;
+            const uint32_t per_step = (uint32_t)NT * Bq * 4u, step_stride = (uint32_t)NT * (uint32_t)a.zBp * 4u;
             const uint32_t nthr = (gridDim.x - (uint32_t)a.zgen_b0) * (NW * 64u);
             const uint32_t me = (blockIdx.x - (uint32_t)a.zgen_b0) * (NW * 64u) + (threadIdx.x - NW * 64u);
             uint64_t gkey[kGI];
-            uint32_t gquad[kGI];
+            uint32_t gquad[kGI], goff[kGI];
 #pragma unroll
             for (int k = 0; k < kGI; ++k) {
                 const uint32_t i = me + (uint32_t)k * nthr;
-                const uint32_t bq = (i >> 2) % (uint32_t)a.zBp, tq = (i >> 2) / (uint32_t)a.zBp;
+                const uint32_t bq = (i >> 2) % Bq, tq = (i >> 2) / Bq;
                 gquad[k] = 4u * tq + (i & 3u);
+                goff[k] = (tq * (uint32_t)a.zBp + bq) * 4u + (i & 3u);
                 gkey[k] = i < per_step ? a.keys[bq < (uint32_t)a.B ? bq : a.B - 1] : 0;
             }
             __builtin_amdgcn_s_barrier();
-            float4* zo = a.zbuf_next + me;
+            float4* zo = a.zbuf_next;
             for (int s = 0; s < a.nsteps; ++s) {
                 if (s < a.zgen_K) {
 #pragma unroll
@@ -503,10 +509,10 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
                         if (me + (uint32_t)k * nthr < per_step) {
                             f2v zp[2];
                             quad_normals_pk((uint64_t)(a.zgen_step0 + s), gquad[k], gkey[k], zp);
-                            zo[(size_t)k * nthr] = make_float4(zp[0].x, zp[0].y, zp[1].x, zp[1].y);
+                            zo[goff[k]] = make_float4(zp[0].x, zp[0].y, zp[1].x, zp[1].y);
                         }
                     }
-                    zo += per_step;
+                    zo += step_stride;
                 }
                 __builtin_amdgcn_s_barrier();
             }
@@ -560,12 +566,15 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         if constexpr (kHalf) return reinterpret_cast<const float2*>(a.zbuf)[q * 2 + (R0 >> 1)];
         else return a.zbuf[q];
     };
+    // V_ZSELF: a one-group workgroup of V_ZPAIR draws its own normals (wave-uniform)
+    const bool zself = kZSelf && (int)blockIdx.x >= a.zgen_b0;
     zt zq[kZD][kZMem ? OT : 1];
     if constexpr (kZMem) {
 #pragma unroll
         for (int d = 0; d < kZD; ++d)
 #pragma unroll
-            for (int u = 0; u < OT; ++u) zq[d][u] = zload(min(d, a.nsteps - 1), u);
+            for (int u = 0; u < OT; ++u)
+                if (!zself) zq[d][u] = zload(min(d, a.nsteps - 1), u);
     }
     // one Euler step; ZS = the V_ZMEM prefetch slot of step s (s % kZD: a compile-time index, so the
     // in-flight normals are never moved between registers -- a move would wait for every older load)
@@ -667,11 +676,13 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         // round trip); issue the load of step s + kZD now (clamped to the block's last step)
         zt zm[kZMem ? OT : 1];
         if constexpr (kZMem) {
-            const int sl = min(s + kZD, a.nsteps - 1);
+            if (!zself) {
+                const int sl = min(s + kZD, a.nsteps - 1);
 #pragma unroll
-            for (int u = 0; u < OT; ++u) {
-                zm[u] = zq[ZS][u];
-                zq[ZS][u] = zload(sl, u);
+                for (int u = 0; u < OT; ++u) {
+                    zm[u] = zq[ZS][u];
+                    zq[ZS][u] = zload(sl, u);
+                }
             }
         }
         // V_ZFIRST: the normals do not depend on the coupling, so they can fill the MFMA chain's gaps
@@ -783,8 +794,12 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             } else if constexpr (kFast && kPk) {
                 f2v zp[2] = {f2v{0, 0}, f2v{0, 0}};
                 if constexpr (kZMem) {
-                    zp[0] = f2v{zm[u].x, zm[u].y};
-                    zp[1] = f2v{zm[u].z, zm[u].w};
+                    if (zself) {
+                        quad_normals_pk(gstep, (uint32_t)(4 * TL(u) + g), key, zp);
+                    } else {
+                        zp[0] = f2v{zm[u].x, zm[u].y};
+                        zp[1] = f2v{zm[u].z, zm[u].w};
+                    }
                 } else if constexpr (kZFirst) {
                     zp[0] = f2v{zz[u][0], zz[u][1]};
                     zp[1] = f2v{zz[u][2], zz[u][3]};
@@ -1148,8 +1163,13 @@ int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int
             const bool rec2 = ka.rec_every > 0 && ka.rec_ld > 0 && ka.rec_ld % 2 == 0 && !ka.recI && !ka.recA &&
                               ((uintptr_t)ka.recE & 7) == 0;
             const int extra = cus - (groups + 1) / 2;
-            rc = rec2 ? launch_v<float, 6, 6, V | V_REC2, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024)
-                      : launch_v<float, 6, 6, V, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024);
+            const char* zs = getenv("WCSDE_ZSELF");
+            if (zs && zs[0] == '1')
+                rc = rec2 ? launch_v<float, 6, 6, V | V_ZSELF | V_REC2, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024)
+                          : launch_v<float, 6, 6, V | V_ZSELF, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024);
+            else
+                rc = rec2 ? launch_v<float, 6, 6, V | V_REC2, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024)
+                          : launch_v<float, 6, 6, V, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024);
         } else {
 #if WC_ZMEM_HALF
         rc = launch_v<float, 6, 12, kVarF32 | X | V_ZMEM | V_HALF2>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);

@@ -775,8 +775,9 @@ __host__ __device__ __forceinline__ uint32_t pimg_unit16(const PGeo& g, int c, i
     return (uint32_t)((((size_t)c * g.SBp + sb) * kPT + t) * 2 + h);
 }
 
-// DIAG (timing ablations only, diag build, WCSDE_PERSISTENT=2..5; results are wrong): 1 = no MFMA,
-// 2 = no epilogue arithmetic, 3 = no remote E-image loads (stale stages), 4 = no hand-off waits
+// DIAG (timing ablations only, diag build, WCSDE_PERSISTENT=2..7; results are wrong): 1 = no MFMA,
+// 2 = no epilogue arithmetic, 3 = no remote E-image loads (stale stages), 4 = no hand-off waits,
+// 5 = half the B-fragment LDS reads (lo part reuses hi), 6 = a fifth of them (tile 0's for all)
 // NRP_T >= 0: the number of remote chunk pairs (NC - 4) / 2 at compile time, the remote K loop
 // fully unrolled (straight-line code keeps the compiler's vmcnt bookkeeping exact: a loop header
 // merges states and waits for every load in flight); -1: a runtime loop, any N
@@ -987,7 +988,10 @@ __global__ void __launch_bounds__(kPWaves * 64, 1) persist_kernel(const PArgs a)
     auto mfma_chunk = [&](f16x8 a0, f16x8 a1, int st, int h, f4 (&acc)[kPT]) {
 #pragma unroll
         for (int t = 0; t < kPT; ++t) {
-            const f16x8 fb0 = ldsB[st][h][t][lane], fb1 = ldsB[st][h][kPT + t][lane];
+            // (DIAG 5: the lo part's B reads skipped, DIAG 6: one simulation tile's fragments for all
+            // five -- the ablations of the LDS read traffic, 8 waves x 10 KB per chunk)
+            const f16x8 fb0 = ldsB[st][h][DIAG == 6 ? 0 : t][lane];
+            const f16x8 fb1 = DIAG == 5 ? fb0 : ldsB[st][h][kPT + (DIAG == 6 ? 0 : t)][lane];
             if (DIAG == 1) {
                 acc[t][0] += (float)fb0[0] + (float)a0[0] + (float)fb1[1] + (float)a1[1];
                 continue;
@@ -1156,7 +1160,7 @@ int cu_count_large() {
 // (libwcsde_diag.so) 2..5 select the timing ablations (wrong results).
 bool persistent_ok(int B, int N) {
     const char* env = getenv("WCSDE_PERSISTENT");
-    if (env && (env[0] < '1' || env[0] > '5')) return false;
+    if (env && (env[0] < '1' || env[0] > '7')) return false;
     const PGeo g = pgeometry(B, N);
     if (2 * (size_t)g.Np * g.Bp * 4 >= (size_t)INT32_MAX) return false;
     int occ = 0;
@@ -1208,6 +1212,8 @@ int run_persistent(const wc_params* p, int B, int N, const double* sc, const dou
         case '3': kern = persist_for<2>(nrp); break;
         case '4': kern = persist_for<3>(nrp); break;
         case '5': kern = persist_for<4>(nrp); break;
+        case '6': kern = persist_for<5>(nrp); break;
+        case '7': kern = persist_for<6>(nrp); break;
         default: break;
     }
 #endif

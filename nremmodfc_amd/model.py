@@ -187,9 +187,10 @@ class Batch:
         rc = L.wc_integrate_status(_lib.ptr(self.ws), self.B, self.N, _PREC[self.precision],
                                    _lib.stream_handle(stream))
         _lib.check(rc, "wc_integrate")
-        if bool(torch.isnan(self.E).any()):
-            why = ("an earlier persistent call's wait timed out, or non-finite inputs (G, sigmaE, initial state)"
-                   if self.N > 96 and self.precision == F32 else "non-finite inputs (G, sigmaE, initial state)")
+        if self.N > 96 and self.precision == F32 and bool(torch.isnan(self.E).any()):
+            # (only the persistent N > 96 path poisons the state; a NaN here can also come from
+            # non-finite inputs)
+            why = "an earlier persistent call's wait timed out, or non-finite inputs (G, sigmaE, initial state)"
             raise _lib.WCSDEError(f"wc_integrate: NaN state ({why})")
 
     def state(self):

@@ -14,6 +14,7 @@ process group, assemble the table from the rank files instead).
 
   python -m nremmodfc_amd.sweep homo      [--seeds 50 --seed0 0] [--grid shipped|script]
   python -m nremmodfc_amd.sweep maps      --map-ids 1 1  [--seeds 25 --seed0 25]
+  python -m nremmodfc_amd.sweep maps      --map-ids 1 1 2 2 --seeds 50 --seed0 0   (C4: both tables, one job)
   python -m nremmodfc_amd.sweep many      --modality homo|map|shuf
   torchrun --nproc-per-node 8 -m nremmodfc_amd.sweep homo ...
 """
@@ -264,28 +265,63 @@ def _rank_world():
 
 def _sim_list(args):
     """The driver's simulation list and output tag (whole_sweep_both.py, _maps.py, run_many_seeds.py)."""
+    jobs = _jobs(args)
+    if len(jobs) != 1:
+        raise SystemExit("this command takes one map-id pair")
+    return jobs[0]
+
+
+def _jobs(args):
+    """[(simulation list, output tag)]: one table per map-id pair.  `maps --map-ids 1 1 2 2` is the
+    C4 job (BASELINE config 4): the real-map and the shuffled-map sweeps as ONE round-robin job over
+    their concatenated lists (whole_sweep_both_maps.py:27-28,92-153 run once per pair), so every rank
+    holds a share of both; each pair is still written to its own table under the reference's name."""
     n = args.nodes
     if args.kind == "homo":
         sims = homogeneous(args.seeds or 50, args.seed0 or 0, args.grid, n)
         tag = args.tag or f"sweep_delta_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_0_0" + (f"_N{n}" if n != 90 else "")
+        jobs = [(sims, tag)]
     elif args.kind == "maps":
-        m1, m2 = args.map_ids
-        sims = maps(m1, m2, args.seeds or 25, 25 if args.seed0 is None else args.seed0, args.grid, n)
-        name = "deltaSHUFFLED" if (m1, m2) == (2, 2) else "deltamaps"
-        tag = args.tag or (f"sweep_{name}_from_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_{m1}_{m2}"
-                           + (f"_N{n}" if n != 90 else ""))
+        ids = list(args.map_ids)
+        if len(ids) % 2 or not ids:
+            raise SystemExit("--map-ids takes pairs: m1 m2 [m1 m2 ...]")
+        pairs = [(ids[i], ids[i + 1]) for i in range(0, len(ids), 2)]
+        if len(set(pairs)) != len(pairs):
+            raise SystemExit("--map-ids: each pair once")
+        if args.tag and len(pairs) > 1:
+            raise SystemExit("--tag names one table: give one map-id pair")
+        jobs = []
+        for m1, m2 in pairs:
+            sims = maps(m1, m2, args.seeds or 25, 25 if args.seed0 is None else args.seed0, args.grid, n)
+            name = "deltaSHUFFLED" if (m1, m2) == (2, 2) else "deltamaps"
+            tag = args.tag or (f"sweep_{name}_from_homoW_fromG{BASE_G}_sigma{BASE_SIGMA}_maps_{m1}_{m2}"
+                               + (f"_N{n}" if n != 90 else ""))
+            jobs.append((sims, tag))
     else:
         sims = many_seeds(args.modality, args.seeds or 50, args.seed0 or 0, n)
         tag = args.tag or f"run_50seeds_output_{args.modality}" + (f"_N{n}" if n != 90 else "")
+        jobs = [(sims, tag)]
     if args.limit:
-        sims = sims[:args.limit]
-    return sims, tag
+        jobs = [(sims[:args.limit], tag) for sims, tag in jobs]
+    return jobs
 
 
-def rank_files_complete(sims, out, tag, world):
-    """True when every rank's TSV file holds its whole round-robin shard."""
+def job_shards(jobs, rank, world):
+    """The round robin over the jobs' concatenated lists: position g (job j's simulation i sits at
+    g = sum of the earlier lists' lengths + i) belongs to rank g % world; for one job, g = i and this
+    is whole_sweep_both.py:63-64's `sim % threads == rank`.  -> [this rank's simulations of job j]."""
+    out, g0 = [], 0
+    for sims, _ in jobs:
+        out.append([s for s in sims if (g0 + s.index) % world == rank])
+        g0 += len(sims)
+    return out
+
+
+def rank_files_complete(sims, out, tag, world, g0=0):
+    """True when every rank's TSV file holds its whole round-robin shard (g0: the list's offset in a
+    multi-table job, job_shards)."""
     for r in range(world):
-        want = {(s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") for s in shard(sims, r, world)}
+        want = {(s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") for s in sims if (g0 + s.index) % world == r}
         if not want <= done_keys(os.path.join(out, "temp", f"{tag}_rank{r}")):
             return False
     return True
@@ -358,7 +394,9 @@ def main(argv=None):
     ap.add_argument("--seeds", type=int, default=None)
     ap.add_argument("--seed0", type=int, default=None)
     ap.add_argument("--grid", default="shipped", choices=("shipped", "script"))
-    ap.add_argument("--map-ids", type=int, nargs=2, default=(1, 1))
+    ap.add_argument("--map-ids", type=int, nargs="+", default=(1, 1),
+                    help="m1 m2 (whole_sweep_both_maps.py:33); several pairs, e.g. 1 1 2 2 with --seeds 50 "
+                         "--seed0 0 (BASELINE config 4), run as one round-robin job writing one table per pair")
     ap.add_argument("--modality", default="map", choices=("homo", "map", "shuf"))
     ap.add_argument("--nodes", type=int, default=90,
                     help="90: the AAL connectome (SC_opti_25julio); other N: the synthetic connectome of "
@@ -375,11 +413,13 @@ def main(argv=None):
 
     if args.kind == "collapse":  # SLURM-array runs: assemble the table once every rank file is complete
         args.kind = args.of
-        sims, tag = _sim_list(args)
         world = args.world or _rank_world()[1]
-        if not rank_files_complete(sims, args.out, tag, world):
-            raise SystemExit(f"collapse: the {world} rank files of {tag} are not complete yet")
-        collapse_sweep(sims, args.out, tag, world)
+        g0 = 0
+        for sims, tag in _jobs(args):
+            if not rank_files_complete(sims, args.out, tag, world, g0):
+                raise SystemExit(f"collapse: the {world} rank files of {tag} are not complete yet")
+            collapse_sweep(sims, args.out, tag, world)
+            g0 += len(sims)
         return
 
     import torch
@@ -397,7 +437,8 @@ def main(argv=None):
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     os.makedirs(os.path.join(args.out, "temp"), exist_ok=True)
-    sims, tag = _sim_list(args)
+    jobs = _jobs(args)
+    sims, tag = jobs[0]
     sched = Schedule(n_trans1=200, n_trans2=2000, n_sim=200_000) if args.short else Schedule()
     if args.nodes == 90:
         empfcs = {s: datasets.load_empfc(s) for s in STATES}
@@ -407,7 +448,8 @@ def main(argv=None):
         sc = datasets.synthetic_sc(args.nodes)
     from .pipeline import check_supported
     check_supported(sc.shape[0], sched)  # fail before integrating, not in the epilogue
-    mine = shard(sims, rank, world)
+    shards = job_shards(jobs, rank, world)
+    mine = shards[0]
 
     if args.kind == "many":
         from . import HMA
@@ -449,33 +491,50 @@ def main(argv=None):
                 pickle.dump(merged, f)
             os.replace(final + f".{os.getpid()}", final)
     else:
-        path = os.path.join(args.out, "temp", f"{tag}_rank{rank}")
-        have = done_keys(path)
-        todo = [s for s in mine if (s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") not in have]
+        # every table of the job in one run: this rank's share of each list, integrated together
+        paths = [os.path.join(args.out, "temp", f"{t}_rank{rank}") for _, t in jobs]
+        todos = []
+        for m, path in zip(shards, paths):
+            have = done_keys(path)
+            todos.append([s for s in m if (s.seed, f"{s.dG:.4f}", f"{s.dsigma:.4f}") not in have])
+        flat = [(k, s) for k, todo in enumerate(todos) for s in todo]
+
+        def on_batch(part, new):
+            for k in range(len(jobs)):
+                sel = [i for i, s in enumerate(part) if owner[id(s)] == k]
+                if sel:
+                    append_rows(paths[k], rank, [part[i] for i in sel], [new[i] for i in sel])
+        owner = {id(s): k for k, s in flat}
         t0 = time.perf_counter()
-        rows, _ = run_sims(todo, sc, empfcs, sched, args.precision, args.batch, device, progress=Progress(rank),
-                           on_batch=lambda part, new: append_rows(path, rank, part, new))
+        rows_all, _ = run_sims([s for _, s in flat], sc, empfcs, sched, args.precision, args.batch, device,
+                               progress=Progress(rank), on_batch=on_batch)
         wall = time.perf_counter() - t0
-        n_steps = len(todo) * sc.shape[0] * sched.n_total
-        perf = json.dumps({"rank": rank, "sims": len(todo), "nodes": sc.shape[0], "wall_s": wall,
+        n_steps = len(flat) * sc.shape[0] * sched.n_total
+        perf = json.dumps({"rank": rank, "sims": len(flat), "nodes": sc.shape[0], "wall_s": wall,
                            "node_steps": n_steps, "node_steps_per_s": n_steps / wall if wall else None,
-                           "batches": getattr(run_sims, "last_timings", None)})
+                           "tables": [t for _, t in jobs], "batches": getattr(run_sims, "last_timings", None)})
         print(perf, flush=True)
-        with open(os.path.join(args.out, "temp", f"{tag}_rank{rank}_perf.jsonl"), "a") as f:  # one line per run
-            f.write(perf + "\n")
-        if dist:  # the data path: every rank's whole shard reaches rank 0 in one all-gather over RCCL
-            gathered = gather_table(shard_table(rank, mine, todo, rows, path), dist, torch.device(device))
-            # every rank holds the whole gathered table: all ranks check it, so they raise together
-            # (a rank-0-only raise would leave the others blocked in the final barrier)
-            if len(gathered) != len(sims):
-                raise RuntimeError(f"gathered {len(gathered)} rows for {len(sims)} simulations")
-            if rank == 0:
-                write_gathered(sims, args.out, tag, gathered)
-        elif launcher == "slurm":
-            if rank_files_complete(sims, args.out, tag, world):  # the last task to finish assembles
+        for path in paths:  # one line per run
+            with open(path + "_perf.jsonl", "a") as f:
+                f.write(perf + "\n")
+        done, g0 = 0, 0
+        for (sims, tag), mine, todo, path in zip(jobs, shards, todos, paths):
+            rows = rows_all[done:done + len(todo)]
+            done += len(todo)
+            if dist:  # the data path: every rank's whole shard reaches rank 0 in one all-gather over RCCL
+                gathered = gather_table(shard_table(rank, mine, todo, rows, path), dist, torch.device(device))
+                # every rank holds the whole gathered table: all ranks check it, so they raise together
+                # (a rank-0-only raise would leave the others blocked in the final barrier)
+                if len(gathered) != len(sims):
+                    raise RuntimeError(f"gathered {len(gathered)} rows for {len(sims)} simulations")
+                if rank == 0:
+                    write_gathered(sims, args.out, tag, gathered)
+            elif launcher == "slurm":
+                if rank_files_complete(sims, args.out, tag, world, g0):  # the last task to finish assembles
+                    collapse_sweep(sims, args.out, tag, world)
+            elif rank == 0:
                 collapse_sweep(sims, args.out, tag, world)
-        elif rank == 0:
-            collapse_sweep(sims, args.out, tag, world)
+            g0 += len(sims)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

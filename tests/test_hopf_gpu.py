@@ -105,8 +105,22 @@ def test_sim_facade_shapes_and_records(cuda):
     oracle.hopf_integrate(p, HM.M, [4], ox, oy, 0, 60)
     rx = oracle.hopf_integrate(p, HM.M, [4], ox, oy, 60, 300, 1)
     assert np.abs(res[:, :, 0] - rx[0]).max() < 1e-10
-    with pytest.raises(NotImplementedError):
-        HM.Hopf_model(None, None, 0)
+    # Hopf_model / Noise alone (Hopf_model_multi.py:46-69): the reference's expression, restated
+    x = x0.reshape(90, 1)
+    y = y0.reshape(90, 1)
+    ones = np.ones((1, 90))
+    dX = (x @ ones).T - (x @ ones)
+    dY = (y @ ones).T - (y @ ones)
+    isx = HM.G * HM.M / HM.norm * dX @ ones.T
+    isy = HM.G * HM.M / HM.norm * dY @ ones.T
+    want = np.hstack(((HM.a - x ** 2 - y ** 2) * x - HM.w * y + isx, (HM.a - x ** 2 - y ** 2) * y + HM.w * x + isy))
+    got = HM.Hopf_model(x, y, 0.0)
+    assert got.shape == (90, 2) and np.abs(got - want).max() <= 1e-13 * np.abs(want).max()
+    HM.set_seed(7)
+    n1 = HM.Noise(x, y, 0.0)
+    HM.set_seed(7)
+    assert np.array_equal(HM.Noise(x, y, 0.0), n1) and n1.shape == (90, 2)
+    assert 0.5 * HM.beta < n1.std() < 1.5 * HM.beta
 
 
 def test_optimizer_iterations_match_oracle_pipeline(cuda):

@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-ARGS="--steps ${PSTEPS:-4} --warmup 1 --no-cpu-baseline"
+ARGS="--steps ${PSTEPS:-4} --warmup 1 --no-cpu-baseline --secondary-steps 0"
 STAMP=$(sha256sum nremmodfc_amd/libwcsde.so | cut -d' ' -f1)  # the library every pass below runs
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o bench -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o p -- python3 bench.py $ARGS > $OUT/fetch.log 2>&1
