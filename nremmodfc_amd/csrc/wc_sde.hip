@@ -255,8 +255,6 @@ enum : int {
                       // (both run the tile's coupling MFMAs; with V_ZMEM, so no Philox is repeated)
     V_F16X6 = 1048576, // A/B: three-part fp16 operands (E and CM each hi + mid + lo), six cross terms
                        // down to 2^-22 (>= 24 significant bits of both operands)
-    V_ZSELF = 2097152, // with V_ZPAIR: the one-group workgroups draw their own normals in-kernel; the
-                       // generators draw only the two-group workgroups' (the first 2 zgen_b0 groups)
     V_ZPAIR = 524288, // SG = 2, V_ZMEM, one workgroup per CU: workgroups < zgen_b0 integrate two groups,
                       // the others one group while their second group's waves draw the next block's
                       // normals, one step's share per step between the workgroup's barriers
@@ -302,7 +300,6 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
     static_assert(!kHalf || (kZMem && kHf && !kHf3), "V_HALF2: the fp16x3 packed path with precomputed normals");
     constexpr bool kZPair = (VAR & V_ZPAIR) != 0;
     static_assert(!kZPair || (kZMem && SG == 2 && NW > 1 && !kHalf), "V_ZPAIR: two groups, normals from zbuf");
-    constexpr bool kZSelf = kZPair && (VAR & V_ZSELF) != 0;
     constexpr float kEsc = kEs ? 1024.0f : 1.0f, kEinv = kEs ? 0x1p-10f : 1.0f;
     // VALU slots after each MFMA in the interleaved schedule (0: compiler's own order)
     constexpr int kIlv = !(kZFirst && kBf && kMfma) ? 0 : (VAR & V_ILV) ? 6 : (VAR & V_ILV2) ? 2 : 0;
@@ -485,9 +482,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             // draws its share of one step of the next block: the same quads every step (key and
             // quad index loaded once), quad_normals_pk and the zbuf layout of zblock_kernel
             constexpr int kGI = 3;  // quads per thread and step at most (host: zpair_shape)
-            // (V_ZSELF: only the simulations of the two-group workgroups, the first Bq of the batch)
-            const uint32_t Bq = kZSelf ? 2u * (uint32_t)a.zgen_b0 * kSims : (uint32_t)a.zBp;
-            const uint32_t per_step = (uint32_t)NT * Bq * 4u, step_stride = (uint32_t)NT * (uint32_t)a.zBp * 4u;
+            const uint32_t Bq = (uint32_t)a.zBp;
+            const uint32_t per_step = (uint32_t)NT * Bq * 4u, step_stride = per_step;
             const uint32_t nthr = (gridDim.x - (uint32_t)a.zgen_b0) * (NW * 64u);
             const uint32_t me = (blockIdx.x - (uint32_t)a.zgen_b0) * (NW * 64u) + (threadIdx.x - NW * 64u);
             uint64_t gkey[kGI];
@@ -566,15 +562,12 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         if constexpr (kHalf) return reinterpret_cast<const float2*>(a.zbuf)[q * 2 + (R0 >> 1)];
         else return a.zbuf[q];
     };
-    // V_ZSELF: a one-group workgroup of V_ZPAIR draws its own normals (wave-uniform)
-    const bool zself = kZSelf && (int)blockIdx.x >= a.zgen_b0;
     zt zq[kZD][kZMem ? OT : 1];
     if constexpr (kZMem) {
 #pragma unroll
         for (int d = 0; d < kZD; ++d)
 #pragma unroll
-            for (int u = 0; u < OT; ++u)
-                if (!zself) zq[d][u] = zload(min(d, a.nsteps - 1), u);
+            for (int u = 0; u < OT; ++u) zq[d][u] = zload(min(d, a.nsteps - 1), u);
     }
     // one Euler step; ZS = the V_ZMEM prefetch slot of step s (s % kZD: a compile-time index, so the
     // in-flight normals are never moved between registers -- a move would wait for every older load)
@@ -676,13 +669,11 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
         // round trip); issue the load of step s + kZD now (clamped to the block's last step)
         zt zm[kZMem ? OT : 1];
         if constexpr (kZMem) {
-            if (!zself) {
-                const int sl = min(s + kZD, a.nsteps - 1);
+            const int sl = min(s + kZD, a.nsteps - 1);
 #pragma unroll
-                for (int u = 0; u < OT; ++u) {
-                    zm[u] = zq[ZS][u];
-                    zq[ZS][u] = zload(sl, u);
-                }
+            for (int u = 0; u < OT; ++u) {
+                zm[u] = zq[ZS][u];
+                zq[ZS][u] = zload(sl, u);
             }
         }
         // V_ZFIRST: the normals do not depend on the coupling, so they can fill the MFMA chain's gaps
@@ -794,12 +785,8 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             } else if constexpr (kFast && kPk) {
                 f2v zp[2] = {f2v{0, 0}, f2v{0, 0}};
                 if constexpr (kZMem) {
-                    if (zself) {
-                        quad_normals_pk(gstep, (uint32_t)(4 * TL(u) + g), key, zp);
-                    } else {
-                        zp[0] = f2v{zm[u].x, zm[u].y};
-                        zp[1] = f2v{zm[u].z, zm[u].w};
-                    }
+                    zp[0] = f2v{zm[u].x, zm[u].y};
+                    zp[1] = f2v{zm[u].z, zm[u].w};
                 } else if constexpr (kZFirst) {
                     zp[0] = f2v{zz[u][0], zz[u][1]};
                     zp[1] = f2v{zz[u][2], zz[u][3]};
@@ -1163,13 +1150,8 @@ int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int
             const bool rec2 = ka.rec_every > 0 && ka.rec_ld > 0 && ka.rec_ld % 2 == 0 && !ka.recI && !ka.recA &&
                               ((uintptr_t)ka.recE & 7) == 0;
             const int extra = cus - (groups + 1) / 2;
-            const char* zs = getenv("WCSDE_ZSELF");
-            if (zs && zs[0] == '1')
-                rc = rec2 ? launch_v<float, 6, 6, V | V_ZSELF | V_REC2, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024)
-                          : launch_v<float, 6, 6, V | V_ZSELF, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024);
-            else
-                rc = rec2 ? launch_v<float, 6, 6, V | V_REC2, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024)
-                          : launch_v<float, 6, 6, V, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024);
+            rc = rec2 ? launch_v<float, 6, 6, V | V_REC2, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024)
+                      : launch_v<float, 6, 6, V, 1, 2>(kb, sc, ws, st, k == 0, extra, 96 * 1024);
         } else {
 #if WC_ZMEM_HALF
         rc = launch_v<float, 6, 12, kVarF32 | X | V_ZMEM | V_HALF2>(kb, sc, ws, st, k == 0, cus - groups, 96 * 1024);
