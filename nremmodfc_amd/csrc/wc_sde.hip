@@ -1136,6 +1136,9 @@ int launch_zmem(const KArgs& ka, const double* sc, void* ws, hipStream_t st, int
         kb.zgen_b0 = PAIR ? groups - cus : groups;  // PAIR: the two-group workgroups come first
         kb.zgen_step0 = kb.step0 + kZK;
         kb.zgen_K = k + 1 < nb ? std::min(kZK, ka.nsteps - (k + 1) * kZK) : 0;
+#ifdef WCSDE_DIAG
+        if (getenv("WCSDE_ZGEN_OFF")) kb.zgen_K = 0;  // timing ablation only: later blocks read stale normals
+#endif
         if (R) {  // this block's first record row (kZK is a multiple of rec_every)
             const size_t row = (size_t)k * kZK / R;
             const size_t off = ka.rec_ld ? row : row * (size_t)ka.B * ka.N;

@@ -40,10 +40,11 @@ def test_abi_version_and_workspace():
     from nremmodfc_amd import _lib
     L = _lib.lib()
     assert L.wcsde_abi_version() == 7
-    # N <= 96: sized for the 3-part 16-bit image (the fp16x2 image and its two scale floats fit inside)
-    assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16
+    # N <= 96: sized for the 3-part 16-bit image and a 256-B slot behind it (the fp16x2 image and its
+    # two scale floats fit inside; the three-part fp16 A/B variant's scales go in the slot)
+    assert L.wc_workspace_size(20000, 90, _lib.WC_F32) == 6 * 3 * 3 * 64 * 16 + 256
     assert L.wc_workspace_size(20000, 90, _lib.WC_F64) == 6 * 6 * 64 * 4 * 8
-    assert L.wc_workspace_size(1, 16, _lib.WC_F32) == 2 * 1 * 3 * 64 * 16
+    assert L.wc_workspace_size(1, 16, _lib.WC_F32) == 2 * 1 * 3 * 64 * 16 + 256
     # N > 96 (wc_sde_large.hip): fp16x2 A image + 2 scale floats (one 256-B slot) + 6 fp32 state arrays
     # (E, I, a_ie pair, G, slope) + 2 fp16x2 E operand images
     Bp, Np = 2560, 1024

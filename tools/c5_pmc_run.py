@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Short C5 integrator run for rocprofv3 --pmc passes (tools/profile_c5_pass.sh): the bench's C5 shard
 (2,500 simulations of the (G, sigma) grid on the 1000-node synthetic connectome), STEPS Euler steps
-recording every 20th into a node-major ring like bench.py --config c5 --sde-only."""
+recording every 20th time-major, as bench.py and the fp32 sweep pipeline record (C5_RING=1: into a
+node-major ring with ld = STEPS / 20, the round-5 harness, whose 4-B record stores at an 80-B stride
+cost partial-line writes)."""
 import os
 import sys
 
@@ -30,8 +32,12 @@ def main():
     G, S, keys = bench.sweep_batch(0)
     G, S, keys = G[:2500], S[:2500], keys[:2500]
     bt = Batch(sc, G, S, keys, driver_params(), precision="f32")
-    ring = torch.empty(2500 * 1000 * (steps // 20), dtype=bt.rec_dtype, device="cuda")
-    bt.integrate(steps, 2.0, 20, ring, rec_ld=steps // 20)
+    if os.environ.get("C5_RING") == "1":
+        ring = torch.empty(2500 * 1000 * (steps // 20), dtype=bt.rec_dtype, device="cuda")
+        bt.integrate(steps, 2.0, 20, ring, rec_ld=steps // 20)
+    else:
+        tmaj = torch.empty((steps // 20, 2500, 1000), dtype=bt.rec_dtype, device="cuda")
+        bt.integrate(steps, 2.0, 20, tmaj)
     torch.cuda.synchronize()
     print("ok", steps)
 

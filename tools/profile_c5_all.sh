@@ -6,7 +6,7 @@
 # failing pass.  Then tools/profile_c5_summary.py on the CPU.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp WCSDE_COOP=0
-for P in ${PASSES:-fetch write sqa sqb tcc}; do
+for P in ${PASSES:-fetch write writering sqa sqb tcc}; do
   bash tools/profile_c5_pass.sh $P || { echo "pass $P failed"; exit 1; }
 done
 # the summaries here (they also land in gpurun_out/prof_c5/), then drop the per-dispatch CSVs, which

@@ -3,7 +3,7 @@
 # dispatch), per gpurun call.  (Round 4's passes segfaulted in process teardown after "tool
 # finalization"; tools/c5_pmc_run.py writes /proc/self/maps at exit to $OUT/<pass>.maps so that the
 # frames of such a fault map to library + offset.)
-#   PASS = fetch | write | sqa | sqb | tcc (L2 hits and misses)  -> gpurun_out/prof_c5/<pass>/ ; then tools/profile_c5_summary.py
+#   PASS = fetch | write | writering | sqa | sqb | tcc (L2 hits and misses)  -> gpurun_out/prof_c5/<pass>/ ; then tools/profile_c5_summary.py
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 P=$1
@@ -12,6 +12,7 @@ mkdir -p $OUT
 case $P in
   fetch) C="FETCH_SIZE" ;;
   write) C="WRITE_SIZE" ;;
+  writering) C="WRITE_SIZE"; export C5_RING=1 ;;  # the round-5 harness's node-major ring records
   sqa) C="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE" ;;
   tcc) C="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" ;;
   sqb) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU GRBM_GUI_ACTIVE" ;;

@@ -23,8 +23,13 @@ def hbm():
     RUN = int(os.environ.get("C5STEPS", "400"))  # one persist_kernel launch integrates RUN steps
     fetch = 2 * vf["FETCH_SIZE"] * 1024.0 / RUN
     write = vw["WRITE_SIZE"] * 1024.0 / RUN
+    Np, Bp = 1024, 2560
+    img = Np * Bp * 4           # the fp16 hi/lo E image every node block publishes each step
+    recs = B * N * 4 / 20       # one fp32 E record per node every 20 steps
     d = {"kernel": kf, "lib_sha256": stamp, "B": B, "N": N, "euler_steps": STEPS, "precision": "f32",
          "fetch_bytes_per_step": fetch, "write_bytes_per_step": write,
+         "write_bytes_per_step_algorithmic": img + recs,
+         "write_excess": write / (img + recs),
          "fetch_bytes_per_launch": fetch * STEPS, "write_bytes_per_launch": write * STEPS,
          "hbm_bytes_per_launch": (fetch + write) * STEPS, "dispatches": vf["dispatches"],
          "state_bytes_per_step": B * N * 36, "connectome_bytes_per_step": 1024 * 1024 * 2 * 2,
@@ -33,6 +38,12 @@ def hbm():
                  "dispatch of 400 Euler steps, divided by 400 and scaled by 20,000 to bench.py's per-chunk 'launch'. FETCH_SIZE x2 (gfx950), KB -> B; the "
                  "counters include Infinity-Cache (MALL) hits; the state stays in registers, so the bytes are the "
                  "per-step operand stream (connectome rows and the E image)."}
+    if os.path.isdir("gpurun_out/prof_c5/writering"):
+        (_, vr), = summary("gpurun_out/prof_c5/writering", "persist_kernel").items()
+        d["write_bytes_per_step_ring_records"] = vr["WRITE_SIZE"] * 1024.0 / RUN
+        d["note_ring"] = ("the round-5 harness recorded into a node-major ring with ld = 20 (4-B stores at an 80-B "
+                          "stride: partial-line writes); bench.py and the fp32 pipeline record time-major, as "
+                          "write_bytes_per_step is measured")
     _dump(d, "pmc_sde_c5.json")
     print(json.dumps(d))
 
