@@ -481,33 +481,35 @@ __global__ void __launch_bounds__(NW * 64 * SG, MINW) wc_sde_kernel(const KArgs 
             // normals stores must not be waited for at every step); between two of them this wave
             // draws its share of one step of the next block: the same quads every step (key and
             // quad index loaded once), quad_normals_pk and the zbuf layout of zblock_kernel
-            constexpr int kGI = 3;  // quads per thread and step at most (host: zpair_shape)
+            constexpr int kGI = 2;  // quads per thread and step at most (host: zpair_shape)
             const uint32_t Bq = (uint32_t)a.zBp;
             const uint32_t per_step = (uint32_t)NT * Bq * 4u, step_stride = per_step;
             const uint32_t nthr = (gridDim.x - (uint32_t)a.zgen_b0) * (NW * 64u);
             const uint32_t me = (blockIdx.x - (uint32_t)a.zgen_b0) * (NW * 64u) + (threadIdx.x - NW * 64u);
             uint64_t gkey[kGI];
             uint32_t gquad[kGI], goff[kGI];
+            bool gon[kGI];
 #pragma unroll
             for (int k = 0; k < kGI; ++k) {
-                const uint32_t i = me + (uint32_t)k * nthr;
+                const uint32_t i0 = me + (uint32_t)k * nthr;
+                gon[k] = i0 < per_step;
+                const uint32_t i = gon[k] ? i0 : 0u;  // (a thread with one quad draws quad 0 twice, stores once)
                 const uint32_t bq = (i >> 2) % Bq, tq = (i >> 2) / Bq;
                 gquad[k] = 4u * tq + (i & 3u);
                 goff[k] = (tq * (uint32_t)a.zBp + bq) * 4u + (i & 3u);
-                gkey[k] = i < per_step ? a.keys[bq < (uint32_t)a.B ? bq : a.B - 1] : 0;
+                gkey[k] = a.keys[bq < (uint32_t)a.B ? bq : a.B - 1];
             }
             __builtin_amdgcn_s_barrier();
             float4* zo = a.zbuf_next;
             for (int s = 0; s < a.nsteps; ++s) {
                 if (s < a.zgen_K) {
+                    // every quad drawn unconditionally (independent Philox chains side by side), stored if owned
+                    f2v zp[kGI][2];
 #pragma unroll
-                    for (int k = 0; k < kGI; ++k) {
-                        if (me + (uint32_t)k * nthr < per_step) {
-                            f2v zp[2];
-                            quad_normals_pk((uint64_t)(a.zgen_step0 + s), gquad[k], gkey[k], zp);
-                            zo[goff[k]] = make_float4(zp[0].x, zp[0].y, zp[1].x, zp[1].y);
-                        }
-                    }
+                    for (int k = 0; k < kGI; ++k) quad_normals_pk((uint64_t)(a.zgen_step0 + s), gquad[k], gkey[k], zp[k]);
+#pragma unroll
+                    for (int k = 0; k < kGI; ++k)
+                        if (gon[k]) zo[goff[k]] = make_float4(zp[k][0].x, zp[k][0].y, zp[k][1].x, zp[k][1].y);
                     zo += step_stride;
                 }
                 __builtin_amdgcn_s_barrier();
@@ -1079,7 +1081,7 @@ size_t zmem_block_bytes(int B) {
 // B and N for which the small-batch path precomputes its normals (fp32, 81 <= N <= 96)
 // V_ZPAIR regime: CUs < groups <= kZPairMax x CUs (the generators, one per one-group workgroup,
 // draw at most ~2.5 quads per thread and step)
-// (1.25: <= 1.67 quads per generator thread and step.  Measured: 4,100 simulations 0.973 us per step
+// (1.25: <= 1.67 quads per generator thread and step, i.e. <= kGI = 2.  Measured: 4,100 simulations 0.973 us per step
 // against 1.138 for the plain two-group kernel, 5,000 1.051 vs 1.144, but 5,700 (357 groups, 2.3
 // quads per thread) 1.181 vs 1.144: the generators set the step; profiles/r06/zpair.log)
 constexpr double kZPairMax = 1.25;
