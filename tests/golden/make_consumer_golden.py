@@ -17,7 +17,8 @@ executes those definitions unmodified in a namespace holding numpy and pandas, a
   (i)  the reference's shipped homogeneous table (output/sweep_delta_homoW_..._9dic24_50iter.txt),
        committed gz'd as tests/golden/shipped_homo_table.csv.gz so the CPU test has the same input;
   (ii) this build's full C3 sweep table (profiles/r06_homo_sweep.txt.gz: 20,000 simulations x the
-       full 1001 s schedule, written by `python -m nremmodfc_amd.sweep homo` on one MI355X);
+       full 1001 s schedule, written by `python -m nremmodfc_amd.sweep homo` on one MI355X), and the
+       C4 job's map and shuffled-map tables (profiles/r06_{maps,shuf}_sweep.txt.gz, 2 x 20,000);
   (iii) this build's C2 pickle (`python -m nremmodfc_amd.sweep many --modality homo`, 200
        simulations with device HMA; our own file, loaded with pickle).
 
@@ -47,6 +48,9 @@ REF = "/root/reference"
 SHIPPED_HOMO = os.path.join(REF, "output", "sweep_delta_homoW_fromG0.16_sigma7.68_maps_0_0_9dic24_50iter.txt")
 SHIPPED_COPY = os.path.join(HERE, "shipped_homo_table.csv.gz")
 PRODUCT_TABLE = os.path.join(ROOT, "profiles", "r06_homo_sweep.txt.gz")
+# the C4 job's two tables (`sweep maps --map-ids 1 1 2 2 --seeds 50 --seed0 0`, one round-robin job)
+PRODUCT_MAPS = os.path.join(ROOT, "profiles", "r06_maps_sweep.txt.gz")
+PRODUCT_SHUF = os.path.join(ROOT, "profiles", "r06_shuf_sweep.txt.gz")
 STATES = ("W", "N1", "N2", "N3")
 
 
@@ -116,7 +120,8 @@ def main():
 
     out = {}
     # extract() reads the file itself (pd.read_csv(filepath), heatmaps.py:31): give it the paths
-    for prefix, path in (("shipped_homo", SHIPPED_COPY), ("product_homo", PRODUCT_TABLE)):
+    for prefix, path in (("shipped_homo", SHIPPED_COPY), ("product_homo", PRODUCT_TABLE),
+                         ("product_maps", PRODUCT_MAPS), ("product_shuf", PRODUCT_SHUF)):
         res = hm["extract"](path)
         out.update(heatmap_fields(prefix, res))
         out[f"{prefix}__sha256"] = np.array(sha256(path))

@@ -8,7 +8,7 @@ heatmaps.py:30-72 ``extract`` and the pickle loaders analyze_many_seeds.py:69-81
 
   * the shipped homogeneous table (tests/golden/shipped_homo_table.csv.gz),
   * this build's full C3 sweep (profiles/r06_homo_sweep.txt.gz: 20,000 simulations x 1001 s on one
-    MI355X, `python -m nremmodfc_amd.sweep homo`),
+    MI355X, `python -m nremmodfc_amd.sweep homo`) and the C4 job's two tables (r06_{maps,shuf}_sweep),
   * this build's C2 pickle (`sweep many --modality homo`, 200 simulations, device HMA),
 
 and committed their outputs (tests/golden/consumer_golden.npz).  The restatements below must give
@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden", "consumer_golden.npz")
 SHIPPED = os.path.join(ROOT, "tests", "golden", "shipped_homo_table.csv.gz")
 PRODUCT = os.path.join(ROOT, "profiles", "r06_homo_sweep.txt.gz")
+PRODUCT_MAPS = os.path.join(ROOT, "profiles", "r06_maps_sweep.txt.gz")   # the C4 job's two tables
+PRODUCT_SHUF = os.path.join(ROOT, "profiles", "r06_shuf_sweep.txt.gz")
 STATES = ("W", "N1", "N2", "N3")
 VAR_EX = {"euccorr": "min", "e": "min", "ssim": "max", "corr": "max"}  # heatmaps.py:23
 THX, THY = (-0.08, 0.2), (-0.2, 0.08)                                  # heatmaps.py:28
@@ -101,6 +103,18 @@ def test_restated_extract_equals_reference_on_shipped_table():
 
 def test_restated_extract_equals_reference_on_this_builds_sweep():
     _check_extract_equals_reference(PRODUCT, "product_homo")
+
+
+def test_restated_extract_equals_reference_on_the_c4_tables():
+    """The C4 job (`sweep maps --map-ids 1 1 2 2 --seeds 50 --seed0 0`) writes the map and the
+    shuffled-map tables; the reference's extract() read both.  On the shuffled table it finds exactly
+    the optima run_many_seeds.py:44-47 quotes, on the map table those of N1 and N2 (:39-42; W and N3
+    sit one or two grid steps away on the flat valley of the published, seed-irreproducible runs)."""
+    maps = _check_extract_equals_reference(PRODUCT_MAPS, "product_maps")
+    shuf = _check_extract_equals_reference(PRODUCT_SHUF, "product_shuf")
+    opt = lambda r: [tuple(float(x) for x in np.round(v[:2], 4)) for v in r["vals_o"][:4]]  # noqa: E731
+    assert opt(shuf) == [(0.0, 0.0), (0.0, 0.04), (0.0, 0.0), (0.0, -0.04)]
+    assert opt(maps)[1:3] == [(0.18, -0.02), (0.02, -0.04)]
 
 
 def test_heatmaps_of_this_builds_sweep_track_the_shipped_ones():
