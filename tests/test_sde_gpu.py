@@ -301,7 +301,8 @@ def test_f32_nonzero_a_ii(cuda, sc90, B):
 
 @pytest.mark.parametrize("N,B,nsteps,ring", [(90, 2500, 2400, False), (90, 161, 4100, True), (90, 37, 2020, False),
                                              (81, 203, 2040, True), (96, 130, 2100, False),
-                                             (90, 5000, 2400, False), (90, 4100, 2040, True), (90, 5100, 3100, True)])
+                                             (90, 5000, 2400, False), (90, 4100, 2040, True), (90, 5100, 3100, True),
+                                             (90, 5120, 2040, False), (81, 4500, 2100, True)])
 def test_small_batch_precomputed_normals_bit_identical(cuda, sc90, N, B, nsteps, ring, monkeypatch):
     """Small batches (strong-scaling shards) draw their normals in blocks on the idle CUs of the same
     launch (V_ZMEM) and run twelve waves per group, half a node tile each (V_HALF2); the trajectory,
@@ -310,7 +311,8 @@ def test_small_batch_precomputed_normals_bit_identical(cuda, sc90, N, B, nsteps,
     counts of the six-tile range (81: the last tile's rows past N masked in both halves).
     B = 4,100 ... 5,100 (257 ... 319 groups, just above one per CU): the two-group workgroups and
     the one-group workgroups whose second group's waves draw the normals (V_ZPAIR) against the
-    in-kernel-noise two-group kernel."""
+    in-kernel-noise two-group kernel; 5,120 = 320 groups is V_ZPAIR's upper edge (1.25 x 256 CUs), and
+    81 nodes at 4,500 the ragged last tile in that regime."""
     from nremmodfc_amd import datasets
     sc = sc90 if N == 90 else datasets.synthetic_sc(N)
     rng = np.random.default_rng(B)
