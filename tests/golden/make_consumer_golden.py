@@ -11,6 +11,9 @@ out with `ast` exactly
                                (``states``, ``var_ex``, ``thx``, ``thy``, heatmaps.py:22-28),
   * analyze_many_seeds.py:69-81 ``load(dic)``          (+ ``states``, :19),
   * figures/Fig5/fig5.py:117-129 ``load(dic, nseeds=50)`` (+ ``states``, :24),
+  * figures/Fig4/new_figure4.py:103-117, the module-level loop that reads the homo, map and shuffled
+    C2 pickles together (+ ``states``, :43) -- top-level statements, not a function, so they are
+    taken out by what they assign,
 
 executes those definitions unmodified in a namespace holding numpy and pandas, and applies them to
 
@@ -19,15 +22,17 @@ executes those definitions unmodified in a namespace holding numpy and pandas, a
   (ii) this build's full C3 sweep table (profiles/r06_homo_sweep.txt.gz: 20,000 simulations x the
        full 1001 s schedule, written by `python -m nremmodfc_amd.sweep homo` on one MI355X), and the
        C4 job's map and shuffled-map tables (profiles/r06_{maps,shuf}_sweep.txt.gz, 2 x 20,000);
-  (iii) this build's C2 pickle (`python -m nremmodfc_amd.sweep many --modality homo`, 200
-       simulations with device HMA; our own file, loaded with pickle).
+  (iii) this build's C2 pickles (`python -m nremmodfc_amd.sweep many --modality homo|map|shuf`,
+       200 simulations each with device HMA; our own files, loaded with pickle).
 
 Only OUTPUTS are committed (plot matrices, optima, violins; matts, Hin_nodes, Hse_nodes) together
 with the sha256 of each input, so tests/test_consumers.py can show that its restatement of these
 functions equals the reference's code on the same inputs, and the -m gpu C2 test can show that
 the engine regenerates the pickle's contents exactly.  No reference source is copied.
 
-  python tests/golden/make_consumer_golden.py --pickle gpurun_out/r06a/many/run_50seeds_output_homo.pickle
+  python tests/golden/make_consumer_golden.py --pickle gpurun_out/r06a/many/run_50seeds_output_homo.pickle \
+      --pickle-map gpurun_out/r06n/many/run_50seeds_output_map.pickle \
+      --pickle-shuf gpurun_out/r06n/many/run_50seeds_output_shuf.pickle
 """
 import argparse
 import ast
@@ -75,6 +80,32 @@ def reference_defs(relpath, funcs, consts):
     return ns
 
 
+def reference_stmts(relpath, names, loop_over):
+    """The top-level statements of a reference script that assign one of `names` (every such
+    assignment, in source order) or loop over `loop_over`, plus its first ``states`` assignment,
+    executed (unchanged) in a namespace with np: for figure scripts whose loaders are module code."""
+    src = open(os.path.join(REF, relpath)).read()
+    tree = ast.parse(src)
+    keep, have_states = [], False
+    for node in tree.body:
+        if isinstance(node, ast.Assign) and len(node.targets) == 1 and isinstance(node.targets[0], ast.Name):
+            name = node.targets[0].id
+            if name == "states" and not have_states:
+                have_states = True
+                keep.append(node)
+            elif name in names:
+                keep.append(node)
+        elif isinstance(node, ast.For) and loop_over in ast.get_source_segment(src, node.iter):
+            keep.append(node)
+    assert have_states and sum(isinstance(n, ast.For) for n in keep) == 1, relpath
+    code = compile(ast.Module(body=keep, type_ignores=[]), os.path.join(REF, relpath), "exec")
+    return code, [ast.get_source_segment(src, n).splitlines()[0] for n in keep]
+
+
+def array_digest(a):
+    return hashlib.sha256(np.ascontiguousarray(np.asarray(a, dtype=np.float64)).tobytes()).hexdigest()
+
+
 def sha256(path):
     h = hashlib.sha256()
     with open(path, "rb") as f:
@@ -106,6 +137,8 @@ def heatmap_fields(prefix, out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pickle", required=True, help="the C2 pickle written by `sweep many --modality homo`")
+    ap.add_argument("--pickle-map", required=True, help="... `--modality map`")
+    ap.add_argument("--pickle-shuf", required=True, help="... `--modality shuf`")
     args = ap.parse_args()
     warnings.filterwarnings("ignore")  # heatmaps.py:18-19 does the same (pandas chained-assignment notes)
 
@@ -135,8 +168,27 @@ def main():
         out[f"c2_homo__{tag}_matts"] = np.stack([matts[s] for s in STATES])
         out[f"c2_homo__{tag}_Hin_nodes"] = np.stack([hin[s] for s in STATES])
         out[f"c2_homo__{tag}_Hse_nodes"] = np.stack([hse[s] for s in STATES])
+
+    # Fig4 (new_figure4.py:94-117): the three pickles read together, keyed by the homo pickle's keys
+    fig4, lines = reference_stmts(os.path.join("figures", "Fig4", "new_figure4.py"),
+                                  {"homo_matts", "map_matts", "shuf_matts"}, "dic_homo")
+    print("fig4 statements:", lines)
+    dics = {}
+    for mod, path in (("map", args.pickle_map), ("shuf", args.pickle_shuf)):
+        with open(path, "rb") as f:  # our own files
+            dics[mod] = pickle.load(f)
+        out[f"c2_{mod}__digest"] = np.array(pickle_digest(dics[mod]))
+    ns = {"np": np, "dic_homo": d, "dic_map": dics["map"], "dic_shuf": dics["shuf"]}
+    exec(fig4, ns)
+    for mod in ("homo", "map", "shuf"):
+        m = np.stack([ns[f"{mod}_matts"][s] for s in STATES])
+        if mod == "homo":  # the same seed means as the loaders above: kept as a digest only
+            assert np.array_equal(m, out["c2_homo__fig5_matts"])
+            out["c2_homo__fig4_matts_sha256"] = np.array(array_digest(m))
+        else:
+            out[f"c2_{mod}__fig4_matts"] = m
     np.savez_compressed(os.path.join(HERE, "consumer_golden.npz"), **out)
-    print("c2 digest", out["c2_homo__digest"])
+    print("c2 digests", out["c2_homo__digest"], out["c2_map__digest"], out["c2_shuf__digest"])
 
 
 if __name__ == "__main__":

@@ -9,11 +9,12 @@ heatmaps.py:30-72 ``extract`` and the pickle loaders analyze_many_seeds.py:69-81
   * the shipped homogeneous table (tests/golden/shipped_homo_table.csv.gz),
   * this build's full C3 sweep (profiles/r06_homo_sweep.txt.gz: 20,000 simulations x 1001 s on one
     MI355X, `python -m nremmodfc_amd.sweep homo`) and the C4 job's two tables (r06_{maps,shuf}_sweep),
-  * this build's C2 pickle (`sweep many --modality homo`, 200 simulations, device HMA),
+  * this build's C2 pickles (`sweep many --modality homo|map|shuf`, 200 simulations each, device HMA),
+    read by those loaders and by Fig4's module-level loop (figures/Fig4/new_figure4.py:103-117),
 
 and committed their outputs (tests/golden/consumer_golden.npz).  The restatements below must give
-those outputs EXACTLY on the same inputs; the -m gpu test regenerates the C2 pickle with the engine
-(deterministic) and checks its contents against the digest of the one the reference's loaders read.
+those outputs EXACTLY on the same inputs; the -m gpu tests regenerate the C2 pickles with the engine
+(deterministic) and checks their contents against the digests of the ones the reference's code read.
 """
 import os
 
@@ -21,7 +22,7 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from tests.golden.make_consumer_golden import pickle_digest, sha256
+from tests.golden.make_consumer_golden import array_digest, pickle_digest, sha256
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden", "consumer_golden.npz")
@@ -136,17 +137,40 @@ def test_heatmaps_of_this_builds_sweep_track_the_shipped_ones():
         assert ours[k][2] <= ship[k][2] * 1.05
 
 
+def fig4_matts(dic_homo, dic_map, dic_shuf):
+    """figures/Fig4/new_figure4.py:103-117 restated: the three C2 pickles read together under the
+    homo pickle's keys; per modality and state the mean over the 50 seeds of sFC."""
+    out = {}
+    for mod, dic in (("homo", dic_homo), ("map", dic_map), ("shuf", dic_shuf)):
+        m = {st: np.zeros((50, 90, 90)) for st in STATES}
+        for key in dic_homo:
+            if key != "metainfo":
+                s, state = key
+                m[state][s] = dic[key]["sFC"]
+        out[mod] = np.stack([m[st].mean(axis=0) for st in STATES])
+    return out
+
+
+@pytest.fixture(scope="module")
+def c2_pickles(tmp_path_factory, cuda):
+    """run_many_seeds.py (C2) through the product on this GPU for the three modalities."""
+    import pickle
+    from nremmodfc_amd import sweep
+    out = str(tmp_path_factory.mktemp("c2"))
+    dics = {}
+    for mod in ("homo", "map", "shuf"):
+        sweep.main(["many", "--modality", mod, "--out", out, "--tag", f"c2{mod}"])
+        with open(os.path.join(out, f"c2{mod}.pickle"), "rb") as f:  # our own file
+            dics[mod] = pickle.load(f)
+    return dics
+
+
 @pytest.mark.gpu
-def test_c2_pickle_regenerates_and_loads_like_the_reference(tmp_path, cuda):
+def test_c2_pickle_regenerates_and_loads_like_the_reference(c2_pickles):
     """run_many_seeds.py (C2, homogeneous optima) through the product on this GPU: the pickle's
     contents equal the pickle the reference's loaders read when the fixture was made (sha256 of
     every array), and the restated loaders give the reference's matts / Hin_nodes / Hse_nodes."""
-    import pickle
-    from nremmodfc_amd import sweep
-    out = str(tmp_path)
-    sweep.main(["many", "--modality", "homo", "--out", out, "--tag", "c2h"])
-    with open(os.path.join(out, "c2h.pickle"), "rb") as f:  # our own file
-        d = pickle.load(f)
+    d = c2_pickles["homo"]
     g = np.load(GOLD)
     assert pickle_digest(d) == str(g["c2_homo__digest"])
     for tag, nseeds in (("asm", None), ("fig5", 50)):
@@ -154,3 +178,19 @@ def test_c2_pickle_regenerates_and_loads_like_the_reference(tmp_path, cuda):
         np.testing.assert_array_equal(np.stack([matts[s] for s in STATES]), g[f"c2_homo__{tag}_matts"])
         np.testing.assert_array_equal(np.stack([hin[s] for s in STATES]), g[f"c2_homo__{tag}_Hin_nodes"])
         np.testing.assert_array_equal(np.stack([hse[s] for s in STATES]), g[f"c2_homo__{tag}_Hse_nodes"])
+
+
+@pytest.mark.gpu
+def test_c2_map_and_shuffled_pickles_load_like_fig4(c2_pickles):
+    """Fig4 (new_figure4.py:94-117) reads the homo, map and shuffled C2 pickles together, indexing
+    the map and shuffled ones with the homo pickle's keys: the regenerated map and shuffled pickles
+    equal the ones the reference's Fig4 statements read (digests), share the homo pickle's keys, and
+    the restated loop gives the reference's seed-mean FCs exactly."""
+    g = np.load(GOLD)
+    for mod in ("map", "shuf"):
+        assert pickle_digest(c2_pickles[mod]) == str(g[f"c2_{mod}__digest"])
+        assert set(c2_pickles[mod]) == set(c2_pickles["homo"])
+    got = fig4_matts(c2_pickles["homo"], c2_pickles["map"], c2_pickles["shuf"])
+    assert array_digest(got["homo"]) == str(g["c2_homo__fig4_matts_sha256"])
+    for mod in ("map", "shuf"):
+        np.testing.assert_array_equal(got[mod], g[f"c2_{mod}__fig4_matts"])
