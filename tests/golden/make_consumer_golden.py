@@ -11,6 +11,10 @@ out with `ast` exactly
                                (``states``, ``var_ex``, ``thx``, ``thy``, heatmaps.py:22-28),
   * analyze_many_seeds.py:69-81 ``load(dic)``          (+ ``states``, :19),
   * figures/Fig5/fig5.py:117-129 ``load(dic, nseeds=50)`` (+ ``states``, :24),
+  * figures/Fig3/new_figure3.py:81-123 ``extract`` (+ ``states``, ``var_ex``, :46-47) on the homo, map
+    and shuffled tables, and its statistics loop :155-164 (Welch-free two-sample t-tests and
+    utils.py:18-22 ``cohen_d`` between the optima's seed distributions; the statsmodels FDR step
+    :165 is left out, statsmodels is not installed),
   * figures/Fig4/new_figure4.py:103-117, the module-level loop that reads the homo, map and shuffled
     C2 pickles together (+ ``states``, :43) -- top-level statements, not a function, so they are
     taken out by what they assign,
@@ -52,6 +56,11 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 SHIPPED_HOMO = os.path.join(REF, "output", "sweep_delta_homoW_fromG0.16_sigma7.68_maps_0_0_9dic24_50iter.txt")
 SHIPPED_COPY = os.path.join(HERE, "shipped_homo_table.csv.gz")
+# the shipped map and shuffled tables (Fig3 reads all three)
+SHIPPED_MAPS = os.path.join(REF, "output", "sweep_deltamaps_from_homoW_fromG0.16_sigma7.68_maps_1_1_9dic24_50iter.txt")
+SHIPPED_SHUF = os.path.join(REF, "output", "sweep_deltaSHUFFLED_from_homoW_fromG0.16_sigma7.68_maps_2_2_9dic24_50iter.txt")
+SHIPPED_MAPS_COPY = os.path.join(HERE, "shipped_maps_table.csv.gz")
+SHIPPED_SHUF_COPY = os.path.join(HERE, "shipped_shuf_table.csv.gz")
 PRODUCT_TABLE = os.path.join(ROOT, "profiles", "r06_homo_sweep.txt.gz")
 # the C4 job's two tables (`sweep maps --map-ids 1 1 2 2 --seeds 50 --seed0 0`, one round-robin job)
 PRODUCT_MAPS = os.path.join(ROOT, "profiles", "r06_maps_sweep.txt.gz")
@@ -80,24 +89,36 @@ def reference_defs(relpath, funcs, consts):
     return ns
 
 
-def reference_stmts(relpath, names, loop_over):
+def shipped_copy(src, dst):
+    if not os.path.exists(dst) or pd.read_csv(dst).shape != pd.read_csv(src).shape:
+        with open(src, "rb") as fi, gzip.GzipFile(dst, "wb", mtime=0) as fo:
+            shutil.copyfileobj(fi, fo)
+    assert pd.read_csv(dst).equals(pd.read_csv(src))
+
+
+def reference_stmts(relpath, names, loop_over, first_only=False, body_has=""):
     """The top-level statements of a reference script that assign one of `names` (every such
-    assignment, in source order) or loop over `loop_over`, plus its first ``states`` assignment,
-    executed (unchanged) in a namespace with np: for figure scripts whose loaders are module code."""
+    assignment in source order, or only the first of each with first_only) or loop over
+    `loop_over` (the first such loop), plus its first ``states`` assignment, compiled unchanged, to
+    be executed in a namespace holding what they read: for figure scripts whose loaders and
+    statistics are module code, not functions."""
     src = open(os.path.join(REF, relpath)).read()
     tree = ast.parse(src)
-    keep, have_states = [], False
+    keep, seen, have_loop = [], set(), False
     for node in tree.body:
         if isinstance(node, ast.Assign) and len(node.targets) == 1 and isinstance(node.targets[0], ast.Name):
             name = node.targets[0].id
-            if name == "states" and not have_states:
-                have_states = True
+            if name == "states" and name not in seen:
+                seen.add(name)
                 keep.append(node)
-            elif name in names:
+            elif name in names and not (first_only and name in seen):
+                seen.add(name)
                 keep.append(node)
-        elif isinstance(node, ast.For) and loop_over in ast.get_source_segment(src, node.iter):
+        elif (isinstance(node, ast.For) and not have_loop and loop_over in ast.get_source_segment(src, node.iter)
+              and body_has in ast.get_source_segment(src, node)):
+            have_loop = True
             keep.append(node)
-    assert have_states and sum(isinstance(n, ast.For) for n in keep) == 1, relpath
+    assert "states" in seen and have_loop and set(names) <= seen, relpath
     code = compile(ast.Module(body=keep, type_ignores=[]), os.path.join(REF, relpath), "exec")
     return code, [ast.get_source_segment(src, n).splitlines()[0] for n in keep]
 
@@ -146,10 +167,8 @@ def main():
     asm = reference_defs("analyze_many_seeds.py", ["load"], ["states"])
     f5 = reference_defs(os.path.join("figures", "Fig5", "fig5.py"), ["load"], ["states"])
 
-    if not os.path.exists(SHIPPED_COPY) or pd.read_csv(SHIPPED_COPY).shape != pd.read_csv(SHIPPED_HOMO).shape:
-        with open(SHIPPED_HOMO, "rb") as fi, gzip.GzipFile(SHIPPED_COPY, "wb", mtime=0) as fo:
-            shutil.copyfileobj(fi, fo)
-    assert pd.read_csv(SHIPPED_COPY).equals(pd.read_csv(SHIPPED_HOMO))
+    for src, dst in ((SHIPPED_HOMO, SHIPPED_COPY), (SHIPPED_MAPS, SHIPPED_MAPS_COPY), (SHIPPED_SHUF, SHIPPED_SHUF_COPY)):
+        shipped_copy(src, dst)
 
     out = {}
     # extract() reads the file itself (pd.read_csv(filepath), heatmaps.py:31): give it the paths
@@ -159,6 +178,29 @@ def main():
         out.update(heatmap_fields(prefix, res))
         out[f"{prefix}__sha256"] = np.array(sha256(path))
         print(prefix, [tuple(np.round(v, 4)) for v in res["vals_o"][:4]])
+
+    # Fig3 (new_figure3.py:142-164): its own extract() on the homo, map and shuffled tables, then the
+    # t-tests and Cohen's d between the optima's seed distributions, state by state
+    from scipy.stats import ttest_ind
+    f3 = reference_defs(os.path.join("figures", "Fig3", "new_figure3.py"), ["extract"], ["states", "var_ex"])
+    ut = reference_defs("utils.py", ["cohen_d"], [])
+    stats_code, stats_lines = reference_stmts(os.path.join("figures", "Fig3", "new_figure3.py"),
+                                              {"p_vals", "cohen_ds"}, "enumerate(states)", first_only=True,
+                                              body_has="ttest(")
+    print("fig3 statements:", stats_lines)
+    for which, paths in (("shipped", (SHIPPED_COPY, SHIPPED_MAPS_COPY, SHIPPED_SHUF_COPY)),
+                         ("product", (PRODUCT_TABLE, PRODUCT_MAPS, PRODUCT_SHUF))):
+        res = [f3["extract"](pth) for pth in paths]
+        for mod, r, pth in zip(("homo", "maps", "shuf"), res, paths):
+            out.update(heatmap_fields(f"fig3_{which}_{mod}", r))
+            out[f"fig3_{which}_{mod}__sha256"] = np.array(sha256(pth))
+        ns = {"np": np, "states": STATES, "ttest": ttest_ind, "utils": argparse.Namespace(cohen_d=ut["cohen_d"]),
+              "output_homo": res[0], "output_map": res[1], "output_shuf": res[2]}
+        exec(stats_code, ns)
+        out[f"fig3_{which}__p_vals"] = np.array(ns["p_vals"])
+        out[f"fig3_{which}__cohen_ds"] = np.array(ns["cohen_ds"])
+        print(which, "fig3 optima", [[tuple(np.round(v[:2], 4)) for v in r["vals_o"][:4]] for r in res])
+        print(which, "fig3 p", np.round(ns["p_vals"], 6), "d", np.round(ns["cohen_ds"], 3))
 
     with open(args.pickle, "rb") as f:  # our own file (written by nremmodfc_amd.sweep)
         d = pickle.load(f)

@@ -3,10 +3,11 @@
 heatmaps.py, analyze_many_seeds.py and figures/Fig5/fig5.py cannot be imported here (seaborn,
 matplotlib, statsmodels and data paths at module top level), and /root/reference does not travel
 to the GPU box.  tests/golden/make_consumer_golden.py therefore ran the REFERENCE's own functions --
-heatmaps.py:30-72 ``extract`` and the pickle loaders analyze_many_seeds.py:69-81 / fig5.py:117-129
+heatmaps.py:30-72 ``extract``, Figure 3's ``extract`` and statistics loop (new_figure3.py:81-123,
+155-164) and the pickle loaders analyze_many_seeds.py:69-81 / fig5.py:117-129
 ``load``, taken out of the sources with ``ast`` and executed unmodified -- on
 
-  * the shipped homogeneous table (tests/golden/shipped_homo_table.csv.gz),
+  * the shipped homogeneous, map and shuffled tables (tests/golden/shipped_{homo,maps,shuf}_table.csv.gz),
   * this build's full C3 sweep (profiles/r06_homo_sweep.txt.gz: 20,000 simulations x 1001 s on one
     MI355X, `python -m nremmodfc_amd.sweep homo`) and the C4 job's two tables (r06_{maps,shuf}_sweep),
   * this build's C2 pickles (`sweep many --modality homo|map|shuf`, 200 simulations each, device HMA),
@@ -27,6 +28,8 @@ from tests.golden.make_consumer_golden import array_digest, pickle_digest, sha25
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden", "consumer_golden.npz")
 SHIPPED = os.path.join(ROOT, "tests", "golden", "shipped_homo_table.csv.gz")
+SHIPPED_MAPS = os.path.join(ROOT, "tests", "golden", "shipped_maps_table.csv.gz")
+SHIPPED_SHUF = os.path.join(ROOT, "tests", "golden", "shipped_shuf_table.csv.gz")
 PRODUCT = os.path.join(ROOT, "profiles", "r06_homo_sweep.txt.gz")
 PRODUCT_MAPS = os.path.join(ROOT, "profiles", "r06_maps_sweep.txt.gz")   # the C4 job's two tables
 PRODUCT_SHUF = os.path.join(ROOT, "profiles", "r06_shuf_sweep.txt.gz")
@@ -65,6 +68,41 @@ def extract(data_pre, xv="delta_G", yv="delta_sigma", var2see="euccorr", C1=0, w
             "violins_o": violins_o}
 
 
+def extract_fig3(data_pre, xv="delta_G", yv="delta_sigma", var2see="euccorr", C1=0, w=1, thx=THX, thy=THY):
+    """figures/Fig3/new_figure3.py:81-123 restated: heatmaps' extract with the grid values rounded
+    to two decimals first (:83-84)."""
+    data_pre = data_pre.copy()
+    data_pre[xv] = np.round(data_pre[xv].values, decimals=2)
+    data_pre[yv] = np.round(data_pre[yv].values, decimals=2)
+    return extract(data_pre, xv, yv, var2see, C1, w, thx, thy)
+
+
+def fig3_stats(out_homo, out_map, out_shuf):
+    """new_figure3.py:155-164 restated: per state, the two-sample t-test p-value and Cohen's d
+    (utils.py:18-22) of homo vs map and shuffled vs map, over the optima's seed distributions."""
+    from scipy.stats import ttest_ind
+    from nremmodfc_amd.utils import cohen_d
+    p, d = [], []
+    for s in range(len(STATES)):
+        h, m, sh = (o["violins_o"][s] for o in (out_homo, out_map, out_shuf))
+        p += [ttest_ind(h, m)[1], ttest_ind(sh, m)[1]]
+        d += [cohen_d(h, m), cohen_d(sh, m)]
+    return np.array(p), np.array(d)
+
+
+def fdr_bh(p):
+    """Benjamini-Hochberg adjusted p-values (statsmodels' multipletests(method='fdr_bh'), which
+    new_figure3.py:165 applies; statsmodels is not installed here, so this step is restated only:
+    parity unpinned)."""
+    p = np.asarray(p, dtype=float)
+    order = np.argsort(p)
+    adj = p[order] * len(p) / np.arange(1, len(p) + 1)
+    adj = np.minimum.accumulate(adj[::-1])[::-1]
+    out = np.empty_like(adj)
+    out[order] = np.minimum(adj, 1.0)
+    return out
+
+
 def load_many_seeds(dic, nseeds=None):
     """analyze_many_seeds.py:69-81 (nseeds from "metainfo") / fig5.py:117-129 (nseeds=50) restated:
     per-state seed-mean FC, and the per-seed nodal integration / segregation."""
@@ -81,10 +119,10 @@ def load_many_seeds(dic, nseeds=None):
     return {st: matts[st].mean(axis=0) for st in STATES}, hin, hse
 
 
-def _check_extract_equals_reference(path, prefix):
+def _check_extract_equals_reference(path, prefix, fn=extract):
     g = np.load(GOLD)
     assert sha256(path) == str(g[f"{prefix}__sha256"]), f"{path} is not the input the reference's extract() read"
-    ours = extract(pd.read_csv(path))
+    ours = fn(pd.read_csv(path))
     np.testing.assert_array_equal(ours["x_vals"], g[f"{prefix}__x_vals"])
     np.testing.assert_array_equal(ours["y_vals"], g[f"{prefix}__y_vals"])
     np.testing.assert_array_equal(np.stack(ours["plotmats"]), g[f"{prefix}__plotmats"])
@@ -116,6 +154,27 @@ def test_restated_extract_equals_reference_on_the_c4_tables():
     opt = lambda r: [tuple(float(x) for x in np.round(v[:2], 4)) for v in r["vals_o"][:4]]  # noqa: E731
     assert opt(shuf) == [(0.0, 0.0), (0.0, 0.04), (0.0, 0.0), (0.0, -0.04)]
     assert opt(maps)[1:3] == [(0.18, -0.02), (0.02, -0.04)]
+
+
+def test_fig3_extract_and_statistics_equal_reference():
+    """Figure 3 (new_figure3.py:138-165) on the shipped homo, map and shuffled tables and on this
+    build's three: the restated extract and t-test / Cohen's d loop equal the reference's code on
+    the same inputs exactly.  On the build's tables, as on the shipped ones, every homo-vs-map and
+    shuffled-vs-map difference of the optima's seed distributions is significant after the FDR step
+    (restated, statsmodels absent) with the same sign of Cohen's d."""
+    g = np.load(GOLD)
+    adj = {}
+    for which, paths in (("shipped", (SHIPPED, SHIPPED_MAPS, SHIPPED_SHUF)),
+                         ("product", (PRODUCT, PRODUCT_MAPS, PRODUCT_SHUF))):
+        res = [_check_extract_equals_reference(pth, f"fig3_{which}_{mod}", extract_fig3)
+               for mod, pth in zip(("homo", "maps", "shuf"), paths)]
+        p, d = fig3_stats(*res)
+        np.testing.assert_array_equal(p, g[f"fig3_{which}__p_vals"])
+        np.testing.assert_array_equal(d, g[f"fig3_{which}__cohen_ds"])
+        adj[which] = (fdr_bh(p), d)
+        print(which, "FDR p", np.round(adj[which][0], 6), "d", np.round(d, 3))
+    assert (adj["shipped"][0] < 0.05).all() and (adj["product"][0] < 0.05).all()
+    np.testing.assert_array_equal(np.sign(adj["product"][1]), np.sign(adj["shipped"][1]))
 
 
 def test_heatmaps_of_this_builds_sweep_track_the_shipped_ones():
