@@ -16,6 +16,9 @@ heatmaps.py:30-72 ``extract``, Figure 3's ``extract`` and statistics loop (new_f
 and committed their outputs (tests/golden/consumer_golden.npz).  The restatements below must give
 those outputs EXACTLY on the same inputs; the -m gpu tests regenerate the C2 pickles with the engine
 (deterministic) and checks their contents against the digests of the ones the reference's code read.
+Fig5's ``corr_HMA`` / ``load_dfs`` (fig5.py:134-198) compare against the shipped empirical pickle
+(output/emp_15inds_output_16dic.pickle): a pickle shipped inside the reference, which no safe loader
+reads, so they are not run; their per-model part is ``load``, pinned above.
 """
 import os
 
