@@ -325,6 +325,38 @@ def test_collapse_orders_rows_like_the_gathered_path(tmp_path):
         assert a.read() == b.read()
 
 
+def test_c4_job_collapse_waits_for_both_tables_rank_files(tmp_path):
+    """A SLURM-array C4 job (`maps --map-ids 1 1 2 2`, no process group): each task writes its share of
+    BOTH tables (the round robin over the concatenated lists, so the shuffled table's shard of rank r
+    starts at global position len(maps list)); `collapse` assembles each table only when every rank
+    file of it holds that shard, and the rank column follows the global round robin."""
+    import pandas as pd
+    out = str(tmp_path)
+    args = sweep.argparse.Namespace(kind="maps", map_ids=[1, 1, 2, 2], seeds=1, seed0=0, grid="shipped", nodes=90,
+                                    tag=None, limit=5)
+    jobs = sweep._jobs(args)
+    os.makedirs(os.path.join(out, "temp"), exist_ok=True)
+
+    def write(rank):
+        for (sims, tag), mine in zip(jobs, sweep.job_shards(jobs, rank, 2)):
+            rows = [{c: s.index + 0.001 * j for j, c in enumerate(sweep.METRIC_COLS)} for s in mine]
+            sweep.append_rows(os.path.join(out, "temp", f"{tag}_rank{rank}"), rank, mine, rows)
+
+    argv = ["collapse", "--of", "maps", "--map-ids", "1", "1", "2", "2", "--seeds", "1", "--seed0", "0",
+            "--limit", "5", "--world", "2", "--out", out]
+    write(0)
+    with pytest.raises(SystemExit):
+        sweep.main(argv)
+    write(1)
+    sweep.main(argv)
+    for k, (sims, tag) in enumerate(jobs):
+        df = pd.read_csv(os.path.join(out, tag + ".txt"))
+        assert len(df) == 5 and list(df.columns) == sweep.HEADER
+        rows = np.load(os.path.join(out, tag + "_rows.npy"))
+        np.testing.assert_array_equal(rows[:, 1], np.arange(5))
+        np.testing.assert_array_equal(rows[:, 0], (np.arange(5) + 5 * k) % 2)  # global position % world
+
+
 def test_slurm_rank_world(monkeypatch):
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setenv("SLURM_ARRAY_TASK_ID", "3")
